@@ -1,0 +1,256 @@
+"""Benchmark of the RAFT-Stereo correlation path on MI355X.
+
+Contract (see task spec): ``python bench.py --gpus N --steps K --warmup W``;
+for N > 1 the driver launches one rank per GPU with torch.distributed.run.
+Rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json configs[1], the metric's config): SceneFlow-size
+540x960 stereo pairs, batch 8 per GPU, 32 GRU iterations, fp32 corr.  One
+"step" = one pass of the hot path over one batch: CorrBlock1D construction
+(volume + fused pyramid, one launch, model.py:366-367) followed by 32 lookups
+(model.py:376), each with its own coordinates, all inputs resident in HBM
+before timing.  Feature maps are synthetic (B, 256, 135, 240) randn (the
+conv2 output shape at 540x960, n_downsample=2); coordinates are
+coords_grid - U[0, 64) per pixel, a fresh draw per iteration.
+
+value = stereo pairs/s through the corr path, all ranks (weak scaling: every
+rank processes its own batch of 8; the path shards by pair with no collective).
+The end-to-end model (encoders/GRU on PyTorch ops) is not in this number.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import pkgload  # noqa: E402
+
+pkgload.load()
+from raft_stereo_amd import CorrBlock1D, coords_grid  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA peak
+
+CONFIGS = {
+    # name: (B per GPU, D, H1, W1, W2, levels, radius, iters, description)
+    "sceneflow": (8, 256, 135, 240, 240, 4, 4, 32,
+                  "corr path: CorrBlock1D build + 32 lookups, 540x960 -> 135x240 fmaps, "
+                  "batch 8/GPU, fp32, 4 levels, radius 4"),
+    "realtime": (1, 256, 120, 160, 160, 3, 4, 7,
+                 "corr path: build + 7 lookups, 480x640 -> 120x160, batch 1, 3 levels"),
+    "middlebury": (1, 256, 496, 720, 720, 4, 4, 32,
+                   "corr path: build + 32 lookups, 1984x2880 -> 496x720, batch 1, fp32"),
+}
+
+
+def lookup_bytes(P, L, r, s_pyr=4):
+    """Algorithmic bytes of one lookup: coords x (4 B) + per level 2r+2 pyramid
+    elements + (2r+1) fp32 outputs, per pixel."""
+    return P * (4 + L * (2 * r + 2) * s_pyr + L * (2 * r + 1) * 4)
+
+
+def volume_flops(B, D, H, W1, W2):
+    return 2.0 * B * H * W1 * W2 * D
+
+
+def volume_bytes(B, D, H, W1, W2, L, s_in=4, s_pyr=4):
+    P = B * H * W1
+    return 2 * B * D * H * W1 * s_in + sum(P * (W2 >> l) * s_pyr for l in range(L + 1))
+
+
+def make_inputs(cfg, device, seed):
+    B, D, H, W1, W2, L, r, iters, _ = cfg
+    g = torch.Generator().manual_seed(seed)
+    f1 = torch.randn(B, D, H, W1, generator=g).to(device)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(device)
+    grid = coords_grid(B, H, W1)
+    coords = []
+    for it in range(iters):
+        gi = torch.Generator().manual_seed(seed * 1000 + it + 1)
+        c = grid.clone()
+        c[:, 0] -= torch.rand(B, H, W1, generator=gi) * 64.0
+        coords.append(c.to(device))
+    return f1, f2, coords
+
+
+def cpu_baseline(cfg, seconds_target=15.0):
+    """Time the oracle's ATen-sequence restatement of model.py:267-326
+    (oracle/torch_ref.py) on this host: one pair (B=1) of the same workload."""
+    from oracle import torch_ref
+    B, D, H, W1, W2, L, r, iters, _ = cfg
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    torch.set_num_threads(cores)
+    f1, f2, coords = make_inputs((1,) + cfg[1:], "cpu", seed=7)
+    blk = torch_ref.TorchCorrBlock1D(f1, f2, L, r)   # warm-up (allocator, threads)
+    blk(coords[0])
+    times = []
+    t_end = time.perf_counter() + seconds_target
+    reps = 0
+    while reps < 1 or (time.perf_counter() < t_end and reps < 5):
+        t0 = time.perf_counter()
+        blk = torch_ref.TorchCorrBlock1D(f1, f2, L, r)
+        for it in range(iters):
+            blk(coords[it])
+        times.append(time.perf_counter() - t0)
+        reps += 1
+    t = sorted(times)[len(times) // 2]
+    cpu_name = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    cpu_name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": 1.0 / t, "unit": "pairs/s", "cores": cores, "kind": "port",
+            "sample": f"1 pair (B=1) of the same workload, build + {iters} lookups via "
+                      f"oracle/torch_ref.py (reference ATen op sequence incl. the torch.unique "
+                      f"assert), median of {len(times)} after 1 warm-up, {cpu_name}",
+            "sec_per_pair": t}
+
+
+def load_traffic(path):
+    try:
+        with open(path) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="sceneflow", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    cfg = CONFIGS[args.config]
+    B, D, H, W1, W2, L, r, iters, desc = cfg
+    f1, f2, coords = make_inputs(cfg, device, seed=1 + rank)
+    P = B * H * W1
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        if ev is not None:
+            ev[1].record()
+        for it in range(iters):
+            out = blk(coords[it])
+        if ev is not None:
+            ev[2].record()
+        return out
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        # kernel-level timing with events on the launch stream (torch's current
+        # stream, which CorrBlock1D launches on)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        lookup_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps / iters
+
+        # per-launch lookup duration without the host gaps between launches:
+        # events around each launch of one extra pass
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
+        for it in range(iters):
+            le[it][0].record()
+            blk(coords[it])
+            le[it][1].record()
+        torch.cuda.synchronize()
+        lookup_launch_ms = sum(a.elapsed_time(b) for a, b in le) / iters
+
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    sec = float(elapsed.item())
+    ms_per_step = 1e3 * sec / args.steps
+    value = world * B * args.steps / sec
+
+    vflops = volume_flops(B, D, H, W1, W2)
+    lbytes = lookup_bytes(P, L, r)
+    traffic = load_traffic(args.traffic).get(args.config, {})
+    roof_volume = {"bound": "mfma", "achieved": vflops / (build_ms * 1e-3) / 1e12,
+                   "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                   "frac": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                   "traffic": traffic.get("build_bytes"),
+                   "algorithmic_bytes": volume_bytes(B, D, H, W1, W2, L),
+                   "kernel": "rc::build_f32_kernel", "avg_launch_us": build_ms * 1e3}
+    lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
+    roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": lgbs / HBM_PEAK_GBS, "traffic": traffic.get("lookup_bytes"),
+                   "algorithmic_bytes": lbytes, "kernel": "rc::lookup_kernel<4,false>",
+                   "avg_launch_us": lookup_launch_ms * 1e3}
+    dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
+
+    result = {
+        "metric": "stereo pairs/s at 540x960, 32 iters, 1-8 GPUs; corr-lookup HBM GB/s",
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (randn fmaps, coords_grid - U[0,64) per iteration)",
+        "config": {"workload": desc, "config": args.config, "global_batch": B * world,
+                   "fmap": [B, D, H, W1], "W2": W2, "levels": L, "radius": r, "iters": iters,
+                   "parallelism": f"batch-shard x{world}"},
+        "roofline": dominant,
+        "roofline_volume": roof_volume,
+        "roofline_lookup": roof_lookup,
+        "lookup_gbs": lgbs,
+        "kernel_ms": {"build": build_ms, "lookup_in_loop": lookup_ms,
+                      "lookup_per_launch": lookup_launch_ms},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+/*
+ * raftcorr.h -- C-ABI of the MI355X (gfx950) correlation path for RAFT-Stereo.
+ *
+ * Drop-in boundary for the reference's CorrBlock1D (/root/reference/model.py):
+ *   rc_corr_build   replaces CorrBlock1D.__init__ + CorrBlock1D.corr
+ *                   (model.py:284-295 and :318-326): all-pairs per-row volume
+ *                   / sqrt(D) plus the avg-pooled pyramid, in one launch.
+ *   rc_corr_pool    replaces one F.avg_pool2d([1,2]) pyramid step (model.py:294);
+ *                   used for levels beyond the fused epilogue (and for A/B runs).
+ *   rc_corr_lookup  replaces CorrBlock1D.__call__ + bilinear_sampler
+ *                   (model.py:297-316 and :267-281).
+ *
+ * The reference has no FFI; its "operator API" is the duck-typed class bound
+ * at model.py:366-367 and called at :376.  raft-stereo_amd/corr.py mirrors that
+ * class on top of these entry points (ctypes).
+ *
+ * Conventions: plain pointers and sizes, device pointers from any allocator
+ * (PyTorch's caching allocator in practice), stream = hipStream_t passed as
+ * void* (NULL = default stream).  Nothing is allocated, nothing synchronises,
+ * nothing throws across the ABI.  Return 0 on success, else an RC_E* code;
+ * rc_last_error() then describes the failure (thread-local).
+ */
+#ifndef RAFTCORR_H
+#define RAFTCORR_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RC_ABI_VERSION 1
+
+/* element types */
+#define RC_F32  0
+#define RC_BF16 1
+
+/* return codes */
+#define RC_OK            0
+#define RC_EINVAL        1  /* bad shape / pointer / alignment / parameter */
+#define RC_EUNSUPPORTED  2  /* valid request this build does not implement */
+#define RC_EHIP          3  /* HIP runtime error (launch / device) */
+
+/* Maximum pyramid buffers one rc_corr_build call writes (num_levels + 1). */
+#define RC_MAX_LEVELS 8
+
+int rc_abi_version(void);
+const char *rc_last_error(void);
+
+/* Volume + pyramid (model.py:284-295, :318-326).
+ *   fmap1: [B][D][H][W1], fmap2: [B][D][H][W2], contiguous, element type
+ *          fmap_dtype (RC_F32, or RC_BF16 for the bf16 MFMA path).
+ *   pyr[l], l < nbuf: device buffers [B*H*W1][W2 >> l] of pyr_dtype; level 0
+ *          is the volume divided by sqrtf(D), level l+1 is the pairwise mean
+ *          of level l along w2 (floor width).  The reference builds
+ *          num_levels+1 buffers (model.py:293); pass nbuf = num_levels + 1.
+ *   Requires (W2 >> (nbuf-1)) >= 1 (the reference raises otherwise) and
+ *   16-byte aligned pointers. */
+int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtype,
+                  int B, int D, int H, int W1, int W2,
+                  void *const *pyr, int nbuf, int pyr_dtype, void *stream);
+
+/* One pooling step (model.py:294): out[p][j] = (in[p][2j] + in[p][2j+1]) / 2,
+ * j < W_in/2, for p < rows.  dtype RC_F32 or RC_BF16 (bf16 rounds once). */
+int rc_corr_pool(const void *in, void *out, long rows, int W_in, int dtype,
+                 void *stream);
+
+/* Lookup (model.py:297-316, :267-281).
+ *   pyr[i], i < levels: [B*H*W1][widths[i]] of pyr_dtype (16-byte aligned).
+ *   coords_x: x channel of the (B,2,H,W1) fp32 coords, element (b,h,w) at
+ *          coords_x[b*coord_batch_stride + h*W1 + w] (the y channel is
+ *          ignored, model.py:299/:308).
+ *   out:   [B][levels*(2*radius+1)][H][W1] fp32, channel = level*(2r+1)+(t+r).
+ *   radius in 1..8, levels in 1..RC_MAX_LEVELS. */
+int rc_corr_lookup(const void *const *pyr, const int *widths, int pyr_dtype,
+                   int levels, int radius, const float *coords_x,
+                   long coord_batch_stride, int B, int H, int W1, float *out,
+                   void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAFTCORR_H */

@@ -1,0 +1,70 @@
+"""ctypes binding of libraftcorr.so (include/raftcorr.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
+raft-stereo_amd/csrc``) into ``raft-stereo_amd/_build/``.  Loading fails
+loudly when it is missing -- the product path has no CPU fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libraftcorr.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
+
+RC_F32, RC_BF16 = 0, 1
+RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
+RC_MAX_LEVELS = 8
+ABI_VERSION = 1
+
+# name -> (restype, argtypes); must match include/raftcorr.h exactly.
+_vp, _i, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+SIGNATURES = {
+    "rc_abi_version": (_i, []),
+    "rc_last_error": (ctypes.c_char_p, []),
+    "rc_corr_build": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i,
+                           ctypes.POINTER(_vp), _i, _i, _vp]),
+    "rc_corr_pool": (_i, [_vp, _vp, _l, _i, _i, _vp]),
+    "rc_corr_lookup": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), _i, _i, _i,
+                            _vp, _l, _i, _i, _i, _vp, _vp]),
+}
+
+_lib = None
+
+
+class CorrLibError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the CDLL; raise if the HIP library is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CorrLibError(
+                f"raft_stereo_amd: HIP library missing at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
+        dll = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(dll, name)
+            fn.restype = res
+            fn.argtypes = args
+        if dll.rc_abi_version() != ABI_VERSION:
+            raise CorrLibError("raft_stereo_amd: libraftcorr ABI version mismatch")
+        _lib = dll
+    return _lib
+
+
+def check(rc, what):
+    if rc != RC_OK:
+        msg = lib().rc_last_error().decode(errors="replace")
+        if rc == RC_EINVAL:
+            raise ValueError(f"{what}: {msg}")
+        raise CorrLibError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+def int_array(vals):
+    return (ctypes.c_int * len(vals))(*vals)

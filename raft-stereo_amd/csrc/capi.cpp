@@ -1,0 +1,143 @@
+// C-ABI entry points declared in include/raftcorr.h.
+//
+// Validation mirrors the reference's failure modes where it has them
+// (e.g. W2 < 2^num_levels makes avg_pool2d raise at model.py:294), then
+// launches on the caller's stream.  Nothing here allocates or synchronises, so
+// every entry point is safe inside hipStreamBeginCapture.
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdint>
+
+#include "../../include/raftcorr.h"
+#include "common.h"
+
+namespace {
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int hip_rc(hipError_t e, const char *what) {
+    if (e == hipSuccess) return RC_OK;
+    return fail(RC_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+bool is_pow2_float(float v) {
+    int e;
+    return std::frexp(v, &e) == 0.5f;
+}
+}  // namespace
+
+extern "C" int rc_abi_version(void) { return RC_ABI_VERSION; }
+
+extern "C" const char *rc_last_error(void) { return g_err; }
+
+extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtype, int B, int D,
+                             int H, int W1, int W2, void *const *pyr, int nbuf, int pyr_dtype,
+                             void *stream) {
+    g_err[0] = 0;
+    if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
+        return fail(RC_EINVAL, "rc_corr_build: bad shape B=%d D=%d H=%d W1=%d W2=%d", B, D, H, W1, W2);
+    if (nbuf < 1 || nbuf > RC_MAX_LEVELS)
+        return fail(RC_EINVAL, "rc_corr_build: nbuf=%d outside 1..%d", nbuf, RC_MAX_LEVELS);
+    if ((W2 >> (nbuf - 1)) < 1)
+        return fail(RC_EINVAL,
+                    "rc_corr_build: pyramid level %d of width %d would be empty "
+                    "(avg_pool2d output size too small, model.py:294)",
+                    nbuf - 1, W2);
+    if (fmap_dtype != RC_F32 && fmap_dtype != RC_BF16)
+        return fail(RC_EINVAL, "rc_corr_build: unknown fmap dtype %d", fmap_dtype);
+    if (pyr_dtype != RC_F32 && pyr_dtype != RC_BF16)
+        return fail(RC_EINVAL, "rc_corr_build: unknown pyramid dtype %d", pyr_dtype);
+    if (fmap_dtype == RC_BF16)
+        return fail(RC_EUNSUPPORTED, "rc_corr_build: bf16 feature maps not built in this version");
+    if (!pyr) return fail(RC_EINVAL, "rc_corr_build: null pyramid array");
+    if ((long long)B * H * W1 == 0) return RC_OK;
+    if (!fmap1 || !fmap2 || !aligned16(fmap1) || !aligned16(fmap2))
+        return fail(RC_EINVAL, "rc_corr_build: feature maps must be non-null and 16-byte aligned");
+    for (int l = 0; l < nbuf; ++l)
+        if (!pyr[l] || !aligned16(pyr[l]))
+            return fail(RC_EINVAL, "rc_corr_build: pyramid buffer %d null or not 16-byte aligned", l);
+
+    rc::BuildArgs a{};
+    a.f1 = fmap1;
+    a.f2 = fmap2;
+    a.B = B; a.D = D; a.H = H; a.W1 = W1; a.W2 = W2;
+    a.nfused = nbuf < 7 ? nbuf : 7;
+    for (int l = 0; l < a.nfused; ++l) a.lvl[l] = pyr[l];
+    a.tiles_m = (W1 + 127) / 128;
+    a.tiles_n = (W2 + 127) / 128;
+    a.sq = std::sqrt((float)D);                 // torch.sqrt(torch.tensor(D).float()), :326
+    a.pow2 = is_pow2_float(a.sq) ? 1 : 0;
+    a.scale = 1.0f / a.sq;                      // exact when pow2
+    a.pyr_bf16 = pyr_dtype == RC_BF16;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc = hip_rc(rc_launch_build_f32(a, s), "rc_corr_build: volume launch");
+    if (rc) return rc;
+    const long rows = (long)B * H * W1;
+    for (int l = a.nfused; l < nbuf; ++l) {
+        rc = hip_rc(rc_launch_pool(pyr[l - 1], pyr[l], rows, W2 >> (l - 1), a.pyr_bf16, s),
+                    "rc_corr_build: pool launch");
+        if (rc) return rc;
+    }
+    return RC_OK;
+}
+
+extern "C" int rc_corr_pool(const void *in, void *out, long rows, int W_in, int dtype,
+                            void *stream) {
+    g_err[0] = 0;
+    if (rows < 0 || W_in < 2)
+        return fail(RC_EINVAL, "rc_corr_pool: bad shape rows=%ld W_in=%d", rows, W_in);
+    if (dtype != RC_F32 && dtype != RC_BF16)
+        return fail(RC_EINVAL, "rc_corr_pool: unknown dtype %d", dtype);
+    if (rows == 0) return RC_OK;
+    if (!in || !out) return fail(RC_EINVAL, "rc_corr_pool: null pointer");
+    return hip_rc(rc_launch_pool(in, out, rows, W_in, dtype == RC_BF16,
+                                 reinterpret_cast<hipStream_t>(stream)),
+                  "rc_corr_pool: launch");
+}
+
+extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, int pyr_dtype, int levels,
+                              int radius, const float *coords_x, long coord_batch_stride, int B,
+                              int H, int W1, float *out, void *stream) {
+    g_err[0] = 0;
+    if (levels < 1 || levels > RC_MAX_LEVELS)
+        return fail(RC_EINVAL, "rc_corr_lookup: levels=%d outside 1..%d", levels, RC_MAX_LEVELS);
+    if (radius < 1 || radius > 8)
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup: radius=%d outside 1..8", radius);
+    if (pyr_dtype != RC_F32 && pyr_dtype != RC_BF16)
+        return fail(RC_EINVAL, "rc_corr_lookup: unknown pyramid dtype %d", pyr_dtype);
+    if (B < 0 || H < 0 || W1 < 0)
+        return fail(RC_EINVAL, "rc_corr_lookup: bad shape B=%d H=%d W1=%d", B, H, W1);
+    if (!pyr || !widths) return fail(RC_EINVAL, "rc_corr_lookup: null pyramid/width array");
+    const long long P = (long long)B * H * W1;
+    if (P == 0) return RC_OK;
+    if ((long long)H * W1 > 0x7FFFFFFF)
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup: H*W1 too large");
+    if (!coords_x || !out) return fail(RC_EINVAL, "rc_corr_lookup: null coords/out");
+    rc::LookupArgs a{};
+    for (int i = 0; i < levels; ++i) {
+        if (widths[i] < 1) return fail(RC_EINVAL, "rc_corr_lookup: level %d width %d", i, widths[i]);
+        if (!pyr[i] || !aligned16(pyr[i]))
+            return fail(RC_EINVAL, "rc_corr_lookup: level %d null or not 16-byte aligned", i);
+        a.lvl[i] = pyr[i];
+        a.W[i] = widths[i];
+    }
+    a.coords = coords_x;
+    a.cbs = coord_batch_stride;
+    a.out = out;
+    a.P = P;
+    a.HW = H * W1;
+    a.levels = levels;
+    return hip_rc(rc_launch_lookup(a, radius, pyr_dtype == RC_BF16,
+                                   reinterpret_cast<hipStream_t>(stream)),
+                  "rc_corr_lookup: launch");
+}

@@ -1,0 +1,72 @@
+// Internal helpers shared by the gfx950 kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rc {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kMaxLevels = 8;
+
+// Raw buffer resource over [base, base + bytes): loads past the end (or at a
+// "negative" offset, which wraps to a huge unsigned one) return 0 and never
+// fault.  Build it from wave-uniform values only (cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes,
+                                             0x00020000);
+}
+
+__device__ __forceinline__ f32x4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0));
+}
+
+__device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0));
+}
+
+__device__ __forceinline__ uint32_t clamp_bytes(long long n) {
+    return n <= 0 ? 0u : (n > 0xFFFFFF00LL ? 0xFFFFFF00u : (uint32_t)n);
+}
+
+// bf16 helpers (round-to-nearest-even; NaN stays NaN via the hardware cvt).
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+    return __builtin_bit_cast(float, (uint32_t)v << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(uint16_t, b);
+}
+
+// Kernel parameter blocks (passed by value).
+struct BuildArgs {
+    const void *f1, *f2;      // [B][D][H][W1], [B][D][H][W2]
+    void *lvl[kMaxLevels];    // pyramid outputs
+    int B, D, H, W1, W2;
+    int nfused;               // levels written by the epilogue (1..7)
+    int tiles_m, tiles_n;     // 128x128 workgroup tiles per (b,h) row
+    float scale;              // exact reciprocal of sqrt(D) when pow2 != 0
+    float sq;                 // sqrtf(D)
+    int pow2;                 // sqrt(D) is a power of two -> multiply is exact
+    int pyr_bf16;             // store pyramid as bf16
+};
+
+struct LookupArgs {
+    const void *lvl[kMaxLevels];
+    int W[kMaxLevels];
+    const float *coords;
+    long long cbs;            // coords batch stride (elements)
+    float *out;
+    long long P;              // B*H*W1
+    int HW;                   // H*W1
+    int levels;
+};
+
+}  // namespace rc
+
+// Host-side launchers (defined in the .hip files, called by capi.cpp).
+hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s);
+hipError_t rc_launch_pool(const void *in, void *out, long rows, int W_in, int bf16,
+                          hipStream_t s);
+hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s);

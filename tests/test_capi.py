@@ -1,0 +1,84 @@
+"""The C-ABI library loads, exports every symbol include/raftcorr.h declares,
+and its host-side validation behaves -- no GPU needed (nothing launches)."""
+import ctypes
+import re
+
+import pytest
+
+import raft_stereo_amd  # noqa: F401  (registered by conftest)
+from raft_stereo_amd import _lib
+
+
+def declared_symbols():
+    text = open(_lib.HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char \*)\s*(rc_\w+)\s*\(", text, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_all_symbols():
+    dll = _lib.lib()
+    for name in declared_symbols():
+        assert hasattr(dll, name), name
+    assert dll.rc_abi_version() == _lib.ABI_VERSION
+
+
+def test_defines_match():
+    text = open(_lib.HEADER).read()
+    for name in ["RC_F32", "RC_BF16", "RC_OK", "RC_EINVAL", "RC_EUNSUPPORTED", "RC_EHIP",
+                 "RC_MAX_LEVELS", "RC_ABI_VERSION"]:
+        m = re.search(rf"#define {name}\s+(\d+)", text)
+        assert m, name
+        ours = getattr(_lib, name if name != "RC_ABI_VERSION" else "ABI_VERSION")
+        assert int(m.group(1)) == ours, name
+
+
+def _build(**kw):
+    args = dict(f1=None, f2=None, dt=0, B=1, D=8, H=1, W1=8, W2=8, pyr=None, nbuf=1, pdt=0)
+    args.update(kw)
+    ptrs = _lib.ptr_array([None] * max(args["nbuf"], 1)) if args["pyr"] is None else args["pyr"]
+    return _lib.lib().rc_corr_build(args["f1"], args["f2"], args["dt"], args["B"], args["D"],
+                                    args["H"], args["W1"], args["W2"], ptrs, args["nbuf"],
+                                    args["pdt"], None)
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(nbuf=0), _lib.RC_EINVAL),
+    (dict(nbuf=9), _lib.RC_EINVAL),
+    (dict(W2=8, nbuf=5), _lib.RC_EINVAL),      # level 4 of width 0 (model.py:294 raises)
+    (dict(D=0), _lib.RC_EINVAL),
+    (dict(dt=7), _lib.RC_EINVAL),
+    (dict(pdt=5), _lib.RC_EINVAL),
+    (dict(dt=1), _lib.RC_EUNSUPPORTED),
+    (dict(), _lib.RC_EINVAL),                   # null feature maps
+])
+def test_build_validation(kw, code):
+    assert _build(**kw) == code
+    assert _lib.lib().rc_last_error()
+
+
+def test_build_empty_is_noop():
+    assert _build(B=0) == _lib.RC_OK
+
+
+def test_lookup_validation():
+    L = _lib.lib()
+    ptrs = _lib.ptr_array([None])
+    w = _lib.int_array([8])
+    assert L.rc_corr_lookup(ptrs, w, 0, 0, 4, None, 0, 1, 1, 8, None, None) == _lib.RC_EINVAL
+    assert L.rc_corr_lookup(ptrs, w, 0, 1, 9, None, 0, 1, 1, 8, None, None) == _lib.RC_EUNSUPPORTED
+    assert L.rc_corr_lookup(ptrs, w, 3, 1, 4, None, 0, 1, 1, 8, None, None) == _lib.RC_EINVAL
+    assert L.rc_corr_lookup(ptrs, w, 0, 1, 4, None, 0, 0, 1, 8, None, None) == _lib.RC_OK
+    # misaligned level pointer is rejected before any launch
+    bad = _lib.ptr_array([ctypes.c_void_p(0x1004)])
+    assert L.rc_corr_lookup(bad, w, 0, 1, 4, ctypes.c_void_p(0x2000), 0, 1, 1, 8,
+                            ctypes.c_void_p(0x3000), None) == _lib.RC_EINVAL
+    assert b"aligned" in L.rc_last_error()
+
+
+def test_pool_validation():
+    L = _lib.lib()
+    assert L.rc_corr_pool(None, None, 4, 1, 0, None) == _lib.RC_EINVAL
+    assert L.rc_corr_pool(None, None, 0, 8, 0, None) == _lib.RC_OK

@@ -1,0 +1,165 @@
+"""Parity of the HIP path (through the C-ABI, via the drop-in CorrBlock1D)
+against the reference goldens and the C oracle.
+
+Tolerances (written here as the contract):
+  * fp32 volume: max|d|/max|ref| <= 1e-4 and rel-L2 <= 1e-5;
+  * pooling: bit-exact given the same level-0 values;
+  * lookup: bit-exact given the same pyramid (NaN == NaN);
+  * bf16 pyramid vs the fp32 oracle: max|d|/max|ref| <= 1e-2, rel-L2 <= 5e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import files, load, norm_err, rel_l2, same
+from oracle import coracle
+from raft_stereo_amd import CorrBlock1D
+from raft_stereo_amd import corr as rcorr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+VOL_TOL, VOL_L2 = 1e-4, 1e-5
+
+
+def cu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def pyr_np(blk):
+    return [t.reshape(t.shape[0], -1).float().cpu().numpy() for t in blk.corr_pyramid]
+
+
+@pytest.mark.parametrize("path", files("volume") + files("lookup"), ids=lambda p: p.split("/")[-1])
+def test_build_vs_golden(path):
+    z = load(path)
+    L = int(z["num_levels"])
+    with torch.no_grad():
+        blk = CorrBlock1D(cu(z["fmap1"]), cu(z["fmap2"]), num_levels=L, radius=4)
+    got = pyr_np(blk)
+    assert len(got) == L + 1
+    assert norm_err(got[0], z["level0"]) <= VOL_TOL
+    assert rel_l2(got[0], z["level0"]) <= VOL_L2
+    for i in range(L):
+        # fused epilogue pooling == avg_pool2d of OUR level i, bit for bit
+        assert same(got[i + 1], coracle.corr_pool(got[i])), f"level {i + 1}"
+        if f"level{i + 1}" in z:
+            assert norm_err(got[i + 1], z[f"level{i + 1}"]) <= VOL_TOL
+
+
+@pytest.mark.parametrize("path", files("lookup"), ids=lambda p: p.split("/")[-1])
+def test_lookup_vs_golden_bitexact(path):
+    """Feed the reference's own pyramid; the HIP lookup must match bit for bit."""
+    z = load(path)
+    L, r = int(z["num_levels"]), int(z["radius"])
+    pyr = [cu(z[f"level{i}"]).view(z[f"level{i}"].shape[0], 1, 1, -1) for i in range(L)]
+    out = rcorr.lookup(pyr, cu(z["coords"]), L, r).cpu().numpy()
+    assert out.shape == z["out"].shape
+    bad = ~((out == z["out"]) | (np.isnan(out) & np.isnan(z["out"])))
+    assert not bad.any(), f"{bad.sum()} mismatches"
+
+
+@pytest.mark.parametrize("path", files("lookup"), ids=lambda p: p.split("/")[-1])
+def test_end_to_end_vs_golden(path):
+    """Build + lookup from the fmaps (volume within tolerance -> lookup too)."""
+    z = load(path)
+    L, r = int(z["num_levels"]), int(z["radius"])
+    with torch.no_grad():
+        blk = CorrBlock1D(cu(z["fmap1"]), cu(z["fmap2"]), num_levels=L, radius=r)
+        out = blk(cu(z["coords"])).cpu().numpy()
+    fin = np.isfinite(z["out"])
+    assert np.array_equal(np.isnan(out), np.isnan(z["out"]))
+    assert norm_err(out[fin], z["out"][fin]) <= VOL_TOL
+    # and bit-exact against the oracle lookup of OUR pyramid
+    ref = coracle.corr_lookup(pyr_np(blk)[:L], z["coords"], L, r)
+    assert same(out, ref)
+
+
+SHAPES = [
+    # B, D, H, W1, W2, L, r
+    (1, 256, 3, 64, 64, 4, 4),
+    (2, 256, 2, 240, 240, 4, 4),    # config-2 row width
+    (1, 256, 2, 311, 311, 4, 4),    # config-3 width (W % 4 != 0)
+    (1, 128, 2, 720, 720, 4, 4),    # config-4 width
+    (1, 37, 3, 37, 53, 4, 3),       # D % 4 != 0, W1 != W2, odd widths
+    (3, 64, 1, 130, 129, 3, 4),     # realtime-style 3 levels, tile tails
+    (1, 16, 1, 20, 600, 7, 2),      # 8 pyramid buffers: fused (7) + pool kernel
+    (1, 32, 2, 33, 64, 2, 8),       # radius 8
+    (1, 32, 2, 40, 50, 1, 1),       # single level, radius 1
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_random_vs_oracle(shape):
+    B, D, H, W1, W2, L, r = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 64
+    x[..., ::7] = torch.randint(-10, W2 + 10, x[..., ::7].shape, generator=g).float()
+    coords = torch.cat([x, torch.randn(B, 1, H, W1, generator=g)], 1)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=r)
+        out = blk(coords.to(DEV)).cpu().numpy()
+    got = pyr_np(blk)
+    ref = coracle.corr_pyramid(f1.numpy(), f2.numpy(), L)
+    assert [a.shape for a in got] == [a.shape for a in ref]
+    assert norm_err(got[0], ref[0]) <= VOL_TOL and rel_l2(got[0], ref[0]) <= VOL_L2
+    for i in range(L):
+        assert same(got[i + 1], coracle.corr_pool(got[i]))
+    assert same(out, coracle.corr_lookup(got[:L], coords.numpy(), L, r))
+
+
+def test_corr_staticmethod():
+    z = load(files("volume")[0])
+    with torch.no_grad():
+        c = CorrBlock1D.corr(cu(z["fmap1"]), cu(z["fmap2"]))
+    B, D, H, W1 = z["fmap1"].shape
+    assert c.shape == (B, H, W1, 1, z["fmap2"].shape[3])
+    assert norm_err(c.reshape(-1, c.shape[-1]).cpu().numpy(), z["level0"]) <= VOL_TOL
+
+
+def test_bf16_pyramid_tolerance():
+    z = load(files("lookup")[1])
+    L, r = int(z["num_levels"]), int(z["radius"])
+    with torch.no_grad():
+        blk = CorrBlock1D(cu(z["fmap1"]), cu(z["fmap2"]), num_levels=L, radius=r,
+                          pyramid_dtype=torch.bfloat16)
+        out = blk(cu(z["coords"])).cpu().numpy()
+    assert blk.corr_pyramid[0].dtype == torch.bfloat16
+    assert norm_err(out, z["out"]) <= 1e-2 and rel_l2(out, z["out"]) <= 5e-3
+
+
+def test_bf16_fmaps_accepted():
+    z = load(files("volume")[1])
+    with torch.no_grad():
+        blk = CorrBlock1D(cu(z["fmap1"]).bfloat16(), cu(z["fmap2"]).bfloat16(), num_levels=4)
+    got = pyr_np(blk)
+    assert norm_err(got[0], z["level0"]) <= 1e-2
+
+
+def test_errors_mirror_reference():
+    f = torch.randn(1, 8, 2, 16, device=DEV)
+    with pytest.raises(RuntimeError):
+        CorrBlock1D(f, torch.randn(1, 8, 2, 9, device=DEV), num_levels=4)  # 9 >> 4 == 0
+    with pytest.raises(RuntimeError):
+        CorrBlock1D(f, torch.randn(1, 8, 3, 16, device=DEV))                # H mismatch
+    blk = CorrBlock1D(f, f, num_levels=2, radius=2)
+    with pytest.raises(RuntimeError):
+        blk(torch.zeros(1, 2, 2, 15, device=DEV))                          # wrong W1
+    with pytest.raises(RuntimeError):
+        blk(torch.zeros(1, 2, 2, 16, device=DEV, dtype=torch.float64))     # dtype
+    fg = f.clone().requires_grad_(True)
+    with pytest.raises(RuntimeError, match="inference-only"):
+        CorrBlock1D(fg, fg)
+
+
+def test_repeat_launches_deterministic():
+    g = torch.Generator().manual_seed(3)
+    f1 = torch.randn(2, 64, 4, 96, generator=g).to(DEV)
+    f2 = torch.randn(2, 64, 4, 96, generator=g).to(DEV)
+    c = (torch.arange(96).float().view(1, 1, 1, 96) - 10 * torch.rand(2, 1, 4, 96, generator=g))
+    c = torch.cat([c, c], 1).to(DEV)
+    with torch.no_grad():
+        outs = [CorrBlock1D(f1, f2)(c) for _ in range(5)]
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
