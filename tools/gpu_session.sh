@@ -1,0 +1,35 @@
+#!/bin/bash
+# One gpurun session: GPU tests, smoke, bench, rocprofv3 kernel trace.
+# Usage (on the GPU box, via gpurun): bash tools/gpu_session.sh <tag> [stages]
+#   stages: comma list of test,smoke,bench,prof (default: all)
+# Every GPU step has its own time limit; a fault/abort/timeout ends the script
+# (exit codes other than 0/1), a plain test failure (1) does not.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}
+STAGES=${2:-test,smoke,bench,prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+has() { [[ ",$STAGES," == *",$1,"* ]]; }
+step() {  # step <name> <timeout> cmd...
+    local name=$1 t=$2; shift 2
+    local t0=$(date +%s)
+    timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "[$name] rc=$rc $(( $(date +%s) - t0 ))s"
+    tail -n 3 "$OUT/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+    return 0
+}
+rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
+has test  && step pytest_gpu 600 python -m pytest tests -m gpu -q -rf
+has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+has bench && step bench 600 python bench.py
+if has prof; then
+    step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace \
+        -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline
+    find "$OUT/prof" -name "*stats*.csv" -exec sh -c 'echo "== $1"; cat "$1"' _ {} \; > "$OUT/kernel_stats.txt" 2>/dev/null
+    head -c 3000 "$OUT/kernel_stats.txt"
+fi
+exit 0
