@@ -216,7 +216,7 @@ def main():
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": lgbs / HBM_PEAK_GBS, "traffic": traffic.get("lookup_bytes"),
-                   "algorithmic_bytes": lbytes, "kernel": "rc::lookup_kernel<4,false>",
+                   "algorithmic_bytes": lbytes, "kernel": "rc::lookup_kernel<4,0,false,true>",
                    "avg_launch_us": lookup_launch_ms * 1e3}
     dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
 

@@ -5,41 +5,123 @@
 //
 // Per (b,h) image row the volume is a GEMM  C[w1][w2] = sum_d F1[d][w1] F2[d][w2]
 // with K = D.  F1/F2 are NCHW, so for a fixed row both operands are "K-major":
-// row d of the operand is W contiguous floats.  v_mfma_f32_16x16x4_f32 takes
-// one f32 per lane for A and for B: lane l supplies A[i=l&15][k=l>>4] and
-// B[k=l>>4][j=l&15].  A lane loads one float4 along w (16 B, so 16 lanes cover
-// 256 contiguous bytes of one d-row and the wave 4 d-rows): component c of that
-// float4 is the operand of the c-th of four 16-wide fragments whose rows are
-// w = w0 + 4*i + c.  The output is therefore "4-interleaved": fragment (ma,nb)
-// register r of lane l holds C[m0 + 4*((l>>4)*4+r) + ma][n0 + 4*(l&15) + nb].
+// row d of an operand is W contiguous floats.  v_mfma_f32_16x16x4_f32 takes one
+// f32 per lane for A and for B: lane l supplies A[i=l&15][k=l>>4] and
+// B[k=l>>4][j=l&15].  A lane loads FM (A) or 4 (B) consecutive floats along w
+// (16 lanes cover one contiguous d-row segment, the wave 4 d-rows); component
+// c of that vector is the operand of the c-th of FM (or 4) 16-wide fragments
+// whose rows are w = w0 + FM*i + c.  The output is therefore interleaved:
+// fragment (ma,nb) register r of lane l holds
+//     C[m0 + FM*((l>>4)*4 + r) + ma][n0 + 4*(l&15) + nb].
 // Each lane thus owns 4 consecutive w2 of a row, which makes the first two
 // pooling steps lane-local and the next ones xor-shuffles (l^1, l^2, ...).
 //
 // Workgroup: 256 threads = 4 waves in a 2x2 arrangement of 64x64 wave tiles
-// (a 128x128 tile of one row's volume).  Workgroups are remapped so that all
-// tiles of one (b,h) row run on one XCD (blocks b, b+8, ... share an XCD) and
-// share that XCD's L2 copy of the row's feature maps.
+// (a 128x128 tile of one row's volume).  A wave whose tile has fewer than 64
+// valid w1 rows uses FM = ceil(rows/16) fragments (e.g. 3 for the 48-row tail
+// of W1 = 240), so padding costs at most 15 rows of MFMA work.  Workgroups are
+// remapped so all tiles of one (b,h) row run on one XCD (blocks b, b+8, ...
+// share an XCD) and share that XCD's L2 copy of the row's feature maps.
+//
+// K loop: two named register sets (no copies, static indexing) each holding U
+// k-steps; one set is loading while the other feeds the MFMAs.  K steps past D
+// load zeros (buffer offset pushed out of range), so there are no per-step
+// guards.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace rc {
 
-// Fragment loads: float4 along w at (d, w) of one (b) image, or zero when
-// d >= D (offset pushed out of the buffer's range).
-template <bool VEC>
-__device__ __forceinline__ f32x4 load_frag(__amdgpu_buffer_rsrc_t r, int d, int D, int H, int h,
-                                           int W, int w) {
-    uint32_t off = (uint32_t)(((long long)(d * H + h) * W + w) * 4);
-    if (d >= D) off = 0xFFFFFFF0u;
-    if constexpr (VEC) {
-        return ld4(r, off);
-    } else {
-        f32x4 v;
-        v.x = ld1(r, off);
-        v.y = ld1(r, off + 4);
-        v.z = ld1(r, off + 8);
-        v.w = ld1(r, off + 12);
-        return v;
+// Dev-only ablation flags (RAFTCORR_BUILD_MODE): 1 = no operand loads,
+// 2 = no epilogue stores, 8 = old register epilogue (narrow per-lane stores
+// for levels >= 1).  Product launches use 0.
+enum { kModeNoLoads = 1, kModeNoStores = 2, kModeRegEpilogue = 8, kModeNtStores = 32 };
+
+constexpr int kStageFloats = 64 * 32;  // per-wave LDS staging: one 64x32 fp32 level-1 tile
+
+// Store level l of a wave tile from its LDS staging image [FM*16 rows][64>>l]
+// as whole-row vector stores: VW floats per lane (VW | W2>>l, so every vector
+// is aligned and either fully inside or fully outside the row), 64/(cw/VW)
+// rows per wave instruction.
+template <int FM, int VW, bool NT>
+__device__ __forceinline__ void store_staged(const float *st, int l, void *lvl, int bf16,
+                                             long long rowbase, int m0, int n0, int W1, int W2,
+                                             int lane) {
+    const int cw = 64 >> l, Wl = W2 >> l;
+    constexpr int lvw = VW == 4 ? 2 : (VW == 2 ? 1 : 0);
+    const int llpr = 6 - l - lvw;     // log2(lanes per row)
+    const int rpi = 64 >> llpr;       // rows per instruction
+    const int Rl = lane >> llpr, j = (lane & ((1 << llpr) - 1)) * VW;
+    const int col = (n0 >> l) + j;
+    for (int r0 = 0; r0 < FM * 16; r0 += rpi) {
+        const int R = r0 + Rl;
+        const int w1 = m0 + R;
+        if (R < FM * 16 && w1 < W1 && col < Wl) {
+            const long long g = (rowbase + w1) * Wl + col;
+            const float *src = st + R * cw + j;
+            if (bf16) {
+#pragma unroll
+                for (int c = 0; c < VW; ++c)
+                    reinterpret_cast<uint16_t *>(lvl)[g + c] = f32_to_bf16(src[c]);
+            } else if constexpr (VW == 4) {
+                f32x4 *d = reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(lvl) + g);
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(src);
+                if constexpr (NT) __builtin_nontemporal_store(v, d);
+                else *d = v;
+            } else if constexpr (VW == 2) {
+                *reinterpret_cast<f32x2 *>(reinterpret_cast<float *>(lvl) + g) =
+                    *reinterpret_cast<const f32x2 *>(src);
+            } else {
+                reinterpret_cast<float *>(lvl)[g] = src[0];
+            }
+        }
     }
+}
+
+template <int FM, bool NT>
+__device__ __forceinline__ void store_staged_any(const float *st, int l, void *lvl, int bf16,
+                                                 long long rowbase, int m0, int n0, int W1,
+                                                 int W2, int lane) {
+    const int Wl = W2 >> l, cw = 64 >> l;
+    if (Wl % 4 == 0 && cw >= 4)
+        store_staged<FM, 4, NT>(st, l, lvl, bf16, rowbase, m0, n0, W1, W2, lane);
+    else if (Wl % 2 == 0 && cw >= 2)
+        store_staged<FM, 2, NT>(st, l, lvl, bf16, rowbase, m0, n0, W1, W2, lane);
+    else
+        store_staged<FM, 1, NT>(st, l, lvl, bf16, rowbase, m0, n0, W1, W2, lane);
+}
+
+template <int N>
+struct FragVec;
+template <>
+struct FragVec<4> { typedef f32x4 T; };
+template <>
+struct FragVec<3> { typedef float T __attribute__((ext_vector_type(3))); };
+template <>
+struct FragVec<2> { typedef f32x2 T; };
+template <>
+struct FragVec<1> { typedef float T __attribute__((ext_vector_type(1))); };
+
+// Load N consecutive floats along w at (d, w) of one image, zeros when d >= D.
+template <int N, bool VEC>
+__device__ __forceinline__ typename FragVec<N>::T load_frag(__amdgpu_buffer_rsrc_t r, int d, int D,
+                                                            int H, int h, int W, int w) {
+    typedef typename FragVec<N>::T V;
+    uint32_t off = (uint32_t)(((long long)(d * H + h) * W + w) * 4);
+    if (d >= D) off = 0xFFFFFF00u;
+    V v;
+    if constexpr (VEC && N == 4) {
+        v = ld4(r, off);
+    } else if constexpr (VEC && N == 3) {
+        v = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b96(r, (int)off, 0, 0));
+    } else if constexpr (VEC && N == 2) {
+        v = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+    } else {
+#pragma unroll
+        for (int c = 0; c < N; ++c) v[c] = ld1(r, off + 4 * c);
+    }
+    return v;
 }
 
 __device__ __forceinline__ void store_level(void *lvl, int bf16, long long idx, float v) {
@@ -49,65 +131,69 @@ __device__ __forceinline__ void store_level(void *lvl, int bf16, long long idx, 
         reinterpret_cast<float *>(lvl)[idx] = v;
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a) {
-    // XCD-aware bijective remap (cdna_hip_programming.md §5, "XCD swizzle").
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-    const int T = a.tiles_m * a.tiles_n;
-    const int row = wgid / T, tile = wgid - row * T;
-    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
-    const int b = row / a.H, h = row - b * a.H;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int m0 = tm * 128 + (wave >> 1) * 64;
-    const int n0 = tn * 128 + (wave & 1) * 64;
-    if (m0 >= a.W1 || n0 >= a.W2) return;  // wave-uniform; no barriers below
+template <int FM, int U>
+struct Stage {
+    typename FragVec<FM>::T a[U];
+    f32x4 b[U];
+};
 
+template <int FM, int U, bool VEC, int MODE>
+__device__ __forceinline__ void load_stage(Stage<FM, U> &s, int k0, int kd,
+                                           __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t r2,
+                                           int D, int H, int h, int W1, int W2, int wa, int wb) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if constexpr (MODE & kModeNoLoads) {
+#pragma unroll
+            for (int c = 0; c < FM; ++c) s.a[u][c] = (float)(wa + c + u) * 1e-3f;
+            s.b[u] = f32x4{(float)wb, (float)(wb + 1), (float)(k0 + u), 1.0f} * 1e-3f;
+        } else {
+            s.a[u] = load_frag<FM, VEC>(r1, k0 + 4 * u + kd, D, H, h, W1, wa);
+            s.b[u] = load_frag<4, VEC>(r2, k0 + 4 * u + kd, D, H, h, W2, wb);
+        }
+    }
+}
+
+template <int FM, int U>
+__device__ __forceinline__ void mma_stage(const Stage<FM, U> &s, f32x4 (&acc)[FM][4]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int ma = 0; ma < FM; ++ma)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+                acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(s.a[u][ma], s.b[u][nb],
+                                                                   acc[ma][nb], 0, 0, 0);
+}
+
+template <int FM, int U, bool VEC, int MODE>
+__device__ __forceinline__ void wave_tile(const BuildArgs &a, int row, int b, int h, int m0,
+                                          int n0, int lane, float *stA, float *stB) {
     const int D = a.D, H = a.H, W1 = a.W1, W2 = a.W2;
     const long long img1 = (long long)D * H * W1, img2 = (long long)D * H * W2;
     const auto r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
     const auto r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
+    const int kd = lane >> 4;             // d offset inside a k-step
+    const int wa = m0 + FM * (lane & 15); // this lane's w1 group
+    const int wb = n0 + 4 * (lane & 15);  // this lane's w2 quad
 
-    const int kd = lane >> 4;                  // d offset inside a k-step
-    const int wa = m0 + 4 * (lane & 15);       // this lane's w1 quad
-    const int wb = n0 + 4 * (lane & 15);       // this lane's w2 quad
-
-    f32x4 acc[4][4];
+    f32x4 acc[FM][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    constexpr int U = 4;  // k-steps (of 4) per pipeline stage
-    const int ksteps = (D + 3) >> 2;
-    f32x4 An[U], Bn[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        An[u] = load_frag<VEC>(r1, 4 * u + kd, D, H, h, W1, wa);
-        Bn[u] = load_frag<VEC>(r2, 4 * u + kd, D, H, h, W2, wb);
-    }
-    for (int ks = 0; ks < ksteps; ks += U) {
-        f32x4 Ac[U], Bc[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) { Ac[u] = An[u]; Bc[u] = Bn[u]; }
-        if (ks + U < ksteps) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                An[u] = load_frag<VEC>(r1, 4 * (ks + U + u) + kd, D, H, h, W1, wa);
-                Bn[u] = load_frag<VEC>(r2, 4 * (ks + U + u) + kd, D, H, h, W2, wb);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (ks + u < ksteps) {
-#pragma unroll
-                for (int ma = 0; ma < 4; ++ma)
-#pragma unroll
-                    for (int nb = 0; nb < 4; ++nb)
-                        acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ac[u][ma], Bc[u][nb],
-                                                                           acc[ma][nb], 0, 0, 0);
-            }
+    constexpr int KS = 4 * U;                      // d per stage
+    const int nst = (D + KS - 1) / KS;             // stages (tail stages read zeros)
+    Stage<FM, U> s0, s1;
+    load_stage<FM, U, VEC, MODE>(s0, 0, kd, r1, r2, D, H, h, W1, W2, wa, wb);
+    load_stage<FM, U, VEC, MODE>(s1, KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
+    for (int st = 0; st < nst; st += 2) {
+        mma_stage<FM, U>(s0, acc);
+        if (st + 2 < nst) load_stage<FM, U, VEC, MODE>(s0, (st + 2) * KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
+        if (st + 1 < nst) {
+            mma_stage<FM, U>(s1, acc);
+            if (st + 3 < nst) load_stage<FM, U, VEC, MODE>(s1, (st + 3) * KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
         }
     }
 
@@ -115,11 +201,13 @@ __global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a) {
     const long long rowbase = (long long)row * W1;  // pyramid row of w1 = 0
     const int col = lane & 15;
     const bool bf = a.pyr_bf16 != 0;
+    constexpr bool kStaged = !(MODE & kModeRegEpilogue);
 #pragma unroll
-    for (int ma = 0; ma < 4; ++ma) {
+    for (int ma = 0; ma < FM; ++ma) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int w1 = m0 + 4 * ((lane >> 4) * 4 + r) + ma;
+            const int R = FM * ((lane >> 4) * 4 + r) + ma;  // tile row (w1 - m0)
+            const int w1 = m0 + R;
             const bool rv = w1 < W1;
             const long long p = rowbase + w1;
             float c[4];
@@ -128,11 +216,17 @@ __global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a) {
                 const float v = acc[ma][nb][r];
                 c[nb] = a.pow2 ? v * a.scale : v / a.sq;
             }
-            // level 0
+            if constexpr (MODE & kModeNoStores) {
+                float keep = c[0] + c[1] + c[2] + c[3];
+                asm volatile("" ::"v"(keep));
+                continue;
+            }
+            // level 0: 4 consecutive w2 per lane, 16 lanes = 256 contiguous bytes
             if (rv) {
                 if (!bf && VEC && wb + 3 < W2) {
-                    *reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(a.lvl[0]) + p * W2 + wb) =
-                        f32x4{c[0], c[1], c[2], c[3]};
+                    f32x4 *d = reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(a.lvl[0]) + p * W2 + wb);
+                    if constexpr ((MODE & kModeNtStores) != 0) __builtin_nontemporal_store(f32x4{c[0], c[1], c[2], c[3]}, d);
+                    else *d = f32x4{c[0], c[1], c[2], c[3]};
                 } else {
 #pragma unroll
                     for (int nb = 0; nb < 4; ++nb)
@@ -142,45 +236,120 @@ __global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a) {
             if (a.nfused < 2) continue;
             // level 1: lane-local pairs
             const float e0 = (c[0] + c[1]) * 0.5f, e1 = (c[2] + c[3]) * 0.5f;
-            {
+            if constexpr (kStaged) {
+                // stage into this wave's LDS image [R][32]; stored as whole rows below
+                *reinterpret_cast<f32x2 *>(stA + R * 32 + 2 * col) = f32x2{e0, e1};
+                continue;
+            } else {
                 const int Wl = W2 >> 1, j = wb >> 1;
                 if (rv) {
                     if (j < Wl) store_level(a.lvl[1], bf, p * Wl + j, e0);
                     if (j + 1 < Wl) store_level(a.lvl[1], bf, p * Wl + j + 1, e1);
                 }
-            }
-            if (a.nfused < 3) continue;
-            // level 2: lane-local
-            float f = (e0 + e1) * 0.5f;
-            {
-                const int Wl = W2 >> 2, j = wb >> 2;
-                if (rv && j < Wl) store_level(a.lvl[2], bf, p * Wl + j, f);
-            }
-            // levels 3..6: xor-shuffle across the 16 lanes of this row group
+                if (a.nfused < 3) continue;
+                float f = (e0 + e1) * 0.5f;
+                {
+                    const int Wl2 = W2 >> 2, j2 = wb >> 2;
+                    if (rv && j2 < Wl2) store_level(a.lvl[2], bf, p * Wl2 + j2, f);
+                }
 #pragma unroll
-            for (int l = 3; l < 7; ++l) {
-                if (a.nfused <= l) break;                 // wave-uniform
-                const int m = 1 << (l - 3);               // lane distance
-                const float o = __shfl_xor(f, m);
-                f = (f + o) * 0.5f;
-                const int Wl = W2 >> l, j = wb >> l;
-                if (rv && (col & (2 * m - 1)) == 0 && j < Wl)
-                    store_level(a.lvl[l], bf, p * Wl + j, f);
+                for (int l = 3; l < 7; ++l) {
+                    if (a.nfused <= l) break;                 // wave-uniform
+                    const int m = 1 << (l - 3);               // lane distance
+                    const float o = __shfl_xor(f, m);
+                    f = (f + o) * 0.5f;
+                    const int Wl3 = W2 >> l, j3 = wb >> l;
+                    if (rv && (col & (2 * m - 1)) == 0 && j3 < Wl3)
+                        store_level(a.lvl[l], bf, p * Wl3 + j3, f);
+                }
             }
+        }
+    }
+    if constexpr (kStaged && !(MODE & kModeNoStores)) {
+        if (a.nfused < 2) return;
+        // Levels >= 1 from the wave-private LDS images (in-order LDS within a
+        // wave: no barrier needed).  Level l+1 = pairwise mean of level l,
+        // read back from LDS: the same fp32 ops as the register path.
+        store_staged_any<FM, (MODE & kModeNtStores) != 0>(stA, 1, a.lvl[1], bf, rowbase, m0, n0, W1, W2, lane);
+        float *src = stA, *dst = stB;
+        for (int l = 2; l < a.nfused; ++l) {
+            const int cw = 64 >> l, cwp = 2 * cw;
+            const int lcw = 6 - l;
+            for (int idx = lane; idx < FM * 16 * cw; idx += 64) {
+                const int R = idx >> lcw, j = idx & (cw - 1);
+                const f32x2 pr = *reinterpret_cast<const f32x2 *>(src + R * cwp + 2 * j);
+                dst[R * cw + j] = (pr[0] + pr[1]) * 0.5f;
+            }
+            store_staged_any<FM, (MODE & kModeNtStores) != 0>(dst, l, a.lvl[l], bf, rowbase, m0, n0, W1, W2, lane);
+            float *t = src;
+            src = dst;
+            dst = t;
         }
     }
 }
 
+template <bool VEC, int U, int MODE>
+__global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a, int nwg_total) {
+    // one LDS array (guide §5 trap 4a): per wave an 8 KB + 4 KB ping-pong
+    // staging image for the pooled levels
+    __shared__ __attribute__((aligned(16))) float smem[4][kStageFloats + kStageFloats / 2];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *stA = smem[wave], *stB = smem[wave] + kStageFloats;
+    const int T = a.tiles_m * a.tiles_n;
+    auto tile_body = [&](int v) {
+        // XCD-aware bijective remap (cdna_hip_programming.md §5, "XCD swizzle").
+        const int xcd = v & 7, q = nwg_total >> 3, rr = nwg_total & 7;
+        const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (v >> 3);
+        const int row = wgid / T, tile = wgid - row * T;
+        const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+        const int b = row / a.H, h = row - b * a.H;
+        const int m0 = tm * 128 + (wave >> 1) * 64;
+        const int n0 = tn * 128 + (wave & 1) * 64;
+        if (m0 >= a.W1 || n0 >= a.W2) return;   // wave-uniform; no barriers in this kernel
+        const int rows = a.W1 - m0;             // valid w1 rows of this wave tile
+        if (rows > 48)
+            wave_tile<4, U, VEC, MODE>(a, row, b, h, m0, n0, lane, stA, stB);
+        else if (rows > 32)
+            wave_tile<3, U, VEC, MODE>(a, row, b, h, m0, n0, lane, stA, stB);
+        else if (rows > 16)
+            wave_tile<2, U, VEC, MODE>(a, row, b, h, m0, n0, lane, stA, stB);
+        else
+            wave_tile<1, U, VEC, MODE>(a, row, b, h, m0, n0, lane, stA, stB);
+    };
+    tile_body(blockIdx.x);
+}
+
+template <bool VEC, int U, int MODE>
+static void launch(const BuildArgs &a, unsigned nwg, hipStream_t s) {
+    hipLaunchKernelGGL((build_f32_kernel<VEC, U, MODE>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
+}
+
 }  // namespace rc
 
+// RAFTCORR_BUILD_MODE (dev-only ablation, read per call): flags 1 no operand
+// loads, 2 no epilogue stores, 4 prefetch U=4 (default U=2), 8 register
+// epilogue, 32 non-temporal pyramid stores.  0 = product.
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
     const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     const bool vec = (a.W1 % 4 == 0) && (a.W2 % 4 == 0);
-    if (vec)
-        hipLaunchKernelGGL(rc::build_f32_kernel<true>, dim3((unsigned)nwg), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(rc::build_f32_kernel<false>, dim3((unsigned)nwg), dim3(256), 0, s, a);
+    int mode = 0;
+    if (const char *e = getenv("RAFTCORR_BUILD_MODE")) mode = atoi(e);
+    const unsigned n = (unsigned)nwg;
+    if (!vec) {
+        rc::launch<false, 2, 0>(a, n, s);
+    } else {
+        switch (mode) {
+            case 1: rc::launch<true, 2, 1>(a, n, s); break;
+            case 2: rc::launch<true, 2, 2>(a, n, s); break;
+            case 3: rc::launch<true, 2, 3>(a, n, s); break;
+            case 4: rc::launch<true, 4, 0>(a, n, s); break;
+            case 8: rc::launch<true, 2, 8>(a, n, s); break;
+            case 12: rc::launch<true, 4, 8>(a, n, s); break;
+            case 32: rc::launch<true, 2, 32>(a, n, s); break;
+            default: rc::launch<true, 2, 0>(a, n, s); break;
+        }
+    }
     return hipGetLastError();
 }

@@ -1,0 +1,77 @@
+"""Interleaved A/B timing of kernel variants in ONE process (guide §5.4 rule 24).
+
+    python tools/ablate.py [--config sceneflow] [--rounds 7]
+
+Variants are dev-only env knobs read per launch by libraftcorr:
+RAFTCORR_BUILD_MODE (volume.hip) and RAFTCORR_LOOKUP_VARIANT (lookup.hip).
+Prints median / min microseconds per launch for each variant.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from raft_stereo_amd import CorrBlock1D  # noqa: E402
+from raft_stereo_amd import corr as rcorr  # noqa: E402
+
+
+def time_launches(fn, n):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    ev[0].record()
+    for k in range(n):
+        fn()
+        ev[k + 1].record()
+    torch.cuda.synchronize()
+    return [ev[k].elapsed_time(ev[k + 1]) * 1e3 for k in range(n)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="sceneflow")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--build-modes", default="0,32,8,4,2,1,3")
+    ap.add_argument("--lookup-variants", default="0,1,3")
+    a = ap.parse_args()
+    cfg = bench.CONFIGS[a.config]
+    B, D, H, W1, W2, L, r, iters, _ = cfg
+    dev = torch.device("cuda", 0)
+    res = {}
+    with torch.no_grad():
+        f1, f2, coords = bench.make_inputs(cfg, dev, seed=1)
+        ref_blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        ref_out = ref_blk(coords[0])
+        bm = [int(x) for x in a.build_modes.split(",") if x]
+        lv = [int(x) for x in a.lookup_variants.split(",") if x]
+        for m in bm:  # warm + correctness of product-equivalent modes
+            os.environ["RAFTCORR_BUILD_MODE"] = str(m)
+            blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+            if m in (0, 4, 8, 32):
+                for i in range(L + 1):
+                    assert torch.equal(blk.corr_pyramid[i], ref_blk.corr_pyramid[i]), (m, i)
+        os.environ["RAFTCORR_BUILD_MODE"] = "0"
+        for v in lv:
+            os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
+            out = ref_blk(coords[0])
+            assert torch.equal(out, ref_out), v
+        for rnd in range(a.rounds):
+            for m in bm:
+                os.environ["RAFTCORR_BUILD_MODE"] = str(m)
+                t = time_launches(lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r), 3)
+                res.setdefault(f"build_mode{m}", []).extend(t)
+            os.environ["RAFTCORR_BUILD_MODE"] = "0"
+            for v in lv:
+                os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
+                t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, coords[rnd % iters], L, r), 8)
+                res.setdefault(f"lookup_v{v}", []).extend(t)
+    out = {k: {"median_us": statistics.median(v), "min_us": min(v), "n": len(v)} for k, v in res.items()}
+    print(json.dumps({"config": a.config, "results": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

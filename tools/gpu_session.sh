@@ -26,10 +26,21 @@ rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
 has test  && step pytest_gpu 600 python -m pytest tests -m gpu -q -rf
 has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has bench && step bench 600 python bench.py
+has ablate && step ablate 600 python tools/ablate.py
 if has prof; then
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace \
         -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline
     find "$OUT/prof" -name "*stats*.csv" -exec sh -c 'echo "== $1"; cat "$1"' _ {} \; > "$OUT/kernel_stats.txt" 2>/dev/null
     head -c 3000 "$OUT/kernel_stats.txt"
+fi
+if has pmc; then
+    step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o f \
+        -- python3 tools/probe.py
+    step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o w \
+        -- python3 tools/probe.py
+    step pmc_sq 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES \
+        --output-format csv -d "$OUT/pmc_sq" -o s -- python3 tools/probe.py
+    python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --out "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
+    cat "$OUT/traffic.log"
 fi
 exit 0

@@ -1,0 +1,47 @@
+"""Isolated launches of the corr kernels for rocprofv3 counter runs.
+
+    python tools/probe.py [--config sceneflow] [--iters N]
+
+Launches, in order: a calibration copy (torch clone of a 1 GiB fp32 tensor:
+exactly 1 GiB read + 1 GiB written), N builds (rc::build_f32_kernel) and N
+lookups (rc::lookup_kernel) of bench.py's workload.  tools/pmc_traffic.py turns
+the per-dispatch FETCH_SIZE / WRITE_SIZE into bytes per launch.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from raft_stereo_amd import CorrBlock1D  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="sceneflow")
+    ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--pyr-dtype", default="f32", choices=["f32", "bf16"])
+    a = ap.parse_args()
+    cfg = bench.CONFIGS[a.config]
+    B, D, H, W1, W2, L, r, iters, _ = cfg
+    dev = torch.device("cuda", 0)
+    pdt = torch.float32 if a.pyr_dtype == "f32" else torch.bfloat16
+    with torch.no_grad():
+        big = torch.randn(1 << 28, device=dev)
+        cal = big.clone()   # calibration: 1 GiB read + 1 GiB write
+        del cal
+        f1, f2, coords = bench.make_inputs(cfg, dev, seed=1)
+        blk = None
+        for _ in range(a.iters):
+            blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=pdt)
+        for it in range(a.iters):
+            blk(coords[it % iters])
+        torch.cuda.synchronize()
+    print("probe done")
+
+
+if __name__ == "__main__":
+    main()
