@@ -75,9 +75,9 @@ def _check_fmaps(fmap1, fmap2):
 
 
 def _prep_fmap(f):
-    # fp32 MFMA path consumes fp32; bf16 fmaps are widened here until the
-    # bf16 MFMA variant lands ("bf16").
-    if f.dtype == torch.bfloat16:
+    # fp32 MFMA path consumes fp32; bf16/fp16 fmaps (autocast) are widened
+    # here until the bf16 MFMA variant lands ("bf16").
+    if f.dtype in (torch.bfloat16, torch.float16):
         f = f.float()
     elif f.dtype != torch.float32:
         raise TypeError(f"raft_stereo_amd: unsupported fmap dtype {f.dtype}")
@@ -152,7 +152,8 @@ class CorrBlock1D:
         self.num_levels = num_levels
         self.radius = radius
         if pyramid_dtype is None:
-            pyramid_dtype = torch.bfloat16 if fmap1.dtype == torch.bfloat16 else torch.float32
+            low = fmap1.dtype in (torch.bfloat16, torch.float16)
+            pyramid_dtype = torch.bfloat16 if low else torch.float32
         self.pyramid_dtype = pyramid_dtype
         self.corr_pyramid = build_pyramid(fmap1, fmap2, num_levels + 1, pyramid_dtype)
 

@@ -36,6 +36,17 @@ FIXES = [
 ]
 
 
+# D8: the forward loop ends at model.py:383 with no
+# coordinate update and no return.  Appended after the update_block call:
+# zero the y component, step the coordinates, record the low-res flow.
+D8_ANCHOR = ("net_list, up_mask, delta_flow = self.update_block(net_list, inp_list, corr, flow, "
+             "iter32=self.args.n_gru_layers==3, iter16=self.args.n_gru_layers>=2)\n")
+D8_TAIL = ("            delta_flow[:,1] = 0.0\n"
+           "            coords1 = coords1 + delta_flow\n"
+           "            flow_predictions.append(coords1 - coords0)\n"
+           "        return flow_predictions\n")
+
+
 def load_reference():
     sys.dont_write_bytecode = True
     with open(REF) as fh:
@@ -44,6 +55,8 @@ def load_reference():
     for old, new in FIXES:
         assert text.count(old) == 1, old
         text = text.replace(old, new)
+    assert text.count(D8_ANCHOR) == 1
+    text = text.replace(D8_ANCHOR, D8_ANCHOR + D8_TAIL)
     mod = types.ModuleType("patched_reference")
     exec(compile(text, "patched_reference", "exec"), mod.__dict__)
     return mod, digest
@@ -109,6 +122,52 @@ def lookup_case(ref, name, B, D, H, W1, W2, L, r, seed, special=False):
             "nan_out": int(np.isnan(out.numpy()).sum())}
 
 
+class Args:
+    """The seven attributes model.py reads (SURVEY.md §5 'Config / flags')."""
+    def __init__(self, **kw):
+        self.hidden_dims = [128] * 3
+        self.n_downsample = 2
+        self.n_gru_layers = 3
+        self.corr_levels = 4
+        self.corr_radius = 4
+        self.mixed_precision = False
+        self.slow_fast_gru = False
+        self.__dict__.update(kw)
+
+
+def state_hash(model):
+    h = hashlib.sha256()
+    for k, v in model.state_dict().items():
+        h.update(k.encode())
+        h.update(v.detach().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def stereo_pair(B, H, W, seed, shift=6):
+    g = gen(seed)
+    left = torch.rand(B, 3, H, W + shift, generator=g) * 255.0
+    right = left[..., :W].clone()
+    left = left[..., shift:].contiguous()
+    right = (right + torch.randn(B, 3, H, W, generator=g) * 2.0).clamp(0, 255)
+    return left, right
+
+
+def e2e_case(ref, name, H, W, iters, seed, **kw):
+    args = Args(**kw)
+    torch.manual_seed(0)
+    model = ref.RAFTStereo(args).eval()
+    img1, img2 = stereo_pair(1, H, W, seed)
+    with torch.no_grad():
+        flows = model(img1, img2, iters=iters)
+    disp = torch.stack([f[:, 0] for f in flows], 0).numpy()   # (iters, B, H1, W1)
+    np.savez_compressed(os.path.join(OUT, f"e2e_{name}.npz"), image1=img1.numpy(),
+                        image2=img2.numpy(), disparity=disp, iters=np.int32(iters))
+    return {"kind": "e2e", "H": H, "W": W, "iters": iters, "args": vars(args),
+            "state_sha256": state_hash(model),
+            "n_tensors": len(model.state_dict()),
+            "n_params": int(sum(p.numel() for p in model.parameters()))}
+
+
 def main():
     ref, digest = load_reference()
     torch.set_num_threads(8)
@@ -127,6 +186,11 @@ def main():
     cases["l_w60_L3"] = lookup_case(ref, "w60_L3", 2, 24, 2, 15, 60, 3, 4, 15)
     cases["l_special"] = lookup_case(ref, "special", 1, 16, 2, 16, 45, 4, 4, 16, special=True)
     cases["l_tiny"] = lookup_case(ref, "tiny", 1, 8, 2, 9, 16, 4, 2, 17)
+    cases["e2e_default"] = e2e_case(ref, "default", 64, 96, 12, 21)
+    cases["e2e_sfgru"] = e2e_case(ref, "sfgru", 64, 80, 6, 22, slow_fast_gru=True, corr_levels=3,
+                                  corr_radius=3)
+    cases["e2e_gru2_ds3"] = e2e_case(ref, "gru2_ds3", 96, 128, 5, 23, n_gru_layers=2, n_downsample=3,
+                                     hidden_dims=[96, 96, 96])
     with open(os.path.join(OUT, "manifest.json"), "w") as fh:
         json.dump(manifest, fh, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -1,0 +1,51 @@
+"""The host network (raft_stereo_amd.network) reproduces the reference's module
+tree: seeded init gives the reference's weight hash, and with the oracle's
+CPU correlation block plugged in the forward reproduces the reference's
+per-iteration disparity bit for bit.  CPU only."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import GOLDEN, load, manifest
+from oracle import torch_ref
+from raft_stereo_amd.network import RAFTStereo, StereoArgs
+
+CASES = {k: v for k, v in manifest()["cases"].items() if v["kind"] == "e2e"}
+
+
+def state_hash(model):
+    h = hashlib.sha256()
+    for k, v in model.state_dict().items():
+        h.update(k.encode())
+        h.update(v.detach().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def build(case):
+    torch.manual_seed(0)
+    return RAFTStereo(StereoArgs(**case["args"]), corr_block=torch_ref.TorchCorrBlock1D).eval()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_seeded_weights_match_reference(name):
+    case = CASES[name]
+    model = build(case)
+    assert len(model.state_dict()) == case["n_tensors"]
+    assert sum(p.numel() for p in model.parameters()) == case["n_params"]
+    assert state_hash(model) == case["state_sha256"]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_forward_matches_reference_on_cpu(name):
+    case = CASES[name]
+    z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
+    model = build(case)
+    torch.set_num_threads(8)
+    with torch.no_grad():
+        flows = model(torch.from_numpy(z["image1"]), torch.from_numpy(z["image2"]),
+                      iters=int(z["iters"]))
+    disp = np.stack([f[:, 0].numpy() for f in flows], 0)
+    assert disp.shape == z["disparity"].shape
+    assert np.abs(disp - z["disparity"]).max() <= 1e-5
