@@ -1,0 +1,70 @@
+"""Worker for tests/test_shard_dist.py, spawned per rank (gloo on CPU).
+Kept import-clean: paths are set up before the package is imported."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pairs():
+    import torch
+    from golden_util import GOLDEN, load
+    z = load(f"{GOLDEN}/e2e_default.npz")
+    img1 = torch.from_numpy(z["image1"]).repeat(3, 1, 1, 1)
+    img2 = torch.from_numpy(z["image2"]).repeat(3, 1, 1, 1)
+    img2[1] = torch.flip(img2[1], dims=[-1])          # make the pairs differ
+    return img1, img2
+
+
+def row_case():
+    import torch
+    g = torch.Generator().manual_seed(5)
+    f1 = torch.randn(2, 16, 7, 24, generator=g)
+    f2 = torch.randn(2, 16, 7, 40, generator=g)
+    x = torch.arange(24).float().view(1, 1, 1, 24).expand(2, 1, 7, 24) - 10 * torch.rand(2, 1, 7, 24, generator=g)
+    return f1, f2, torch.cat([x, torch.zeros(2, 1, 7, 24)], 1)
+
+
+def model():
+    import torch
+    import pkgload
+    pkgload.load()
+    from golden_util import manifest
+    from oracle import torch_ref
+    from raft_stereo_amd.network import RAFTStereo, StereoArgs
+    torch.manual_seed(0)
+    case = manifest()["cases"]["e2e_default"]
+    return RAFTStereo(StereoArgs(**case["args"]), corr_block=torch_ref.TorchCorrBlock1D).eval()
+
+
+def run(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import pkgload
+    pkgload.load()
+    from oracle import torch_ref
+    from raft_stereo_amd.shard import RowShardedCorr, gather_batch, local_batch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    try:
+        img1, img2 = pairs()
+        net = model()
+        with torch.no_grad():
+            flows = net(local_batch(img1, rank, world), local_batch(img2, rank, world), iters=3)
+        full = gather_batch(flows[-1], world)
+        f1, f2, coords = row_case()
+        part = RowShardedCorr(f1, f2, rank, world, num_levels=3, radius=3,
+                              corr_block=torch_ref.TorchCorrBlock1D)(coords)
+        parts = [None] * world
+        dist.all_gather_object(parts, part)
+        q.put((rank, full, torch.cat(parts, dim=2) if rank == 0 else None))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e), None))
+    finally:
+        dist.destroy_process_group()
