@@ -42,6 +42,9 @@ CONFIGS = {
     "sceneflow": (8, 256, 135, 240, 240, 4, 4, 32,
                   "corr path: CorrBlock1D build + 32 lookups, 540x960 -> 135x240 fmaps, "
                   "batch 8/GPU, fp32, 4 levels, radius 4"),
+    "kitti": (8, 256, 94, 311, 311, 4, 4, 32,
+              "corr path: build + 32 lookups, 375x1242 -> 94x311 fmaps, batch 8/GPU "
+              "(64 global at 8 GPUs), bf16 fmaps, bf16 MFMA volume + bf16 pyramid"),
     "realtime": (1, 256, 120, 160, 160, 3, 4, 7,
                  "corr path: build + 7 lookups, 480x640 -> 120x160, batch 1, 3 levels"),
     "middlebury": (1, 256, 496, 720, 720, 4, 4, 32,
@@ -64,11 +67,14 @@ def volume_bytes(B, D, H, W1, W2, L, s_in=4, s_pyr=4):
     return 2 * B * D * H * W1 * s_in + sum(P * (W2 >> l) * s_pyr for l in range(L + 1))
 
 
-def make_inputs(cfg, device, seed):
+BF16_CONFIGS = {"kitti"}
+
+
+def make_inputs(cfg, device, seed, dtype=torch.float32):
     B, D, H, W1, W2, L, r, iters, _ = cfg
     g = torch.Generator().manual_seed(seed)
-    f1 = torch.randn(B, D, H, W1, generator=g).to(device)
-    f2 = torch.randn(B, D, H, W2, generator=g).to(device)
+    f1 = torch.randn(B, D, H, W1, generator=g).to(device, dtype)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(device, dtype)
     grid = coords_grid(B, H, W1)
     coords = []
     for it in range(iters):
@@ -120,6 +126,34 @@ def cpu_baseline(cfg, seconds_target=15.0):
             "sec_per_pair": t}
 
 
+def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False):
+    """Whole network (encoders/GRU on PyTorch ops + the HIP corr path) on
+    synthetic pairs at the config's image size: pairs/s and the corr share."""
+    from raft_stereo_amd.network import RAFTStereo, StereoArgs
+    B, D, H1, W1, W2, L, r, iters, _ = cfg
+    torch.manual_seed(0)
+    args = StereoArgs(corr_levels=L, corr_radius=r, mixed_precision=mixed)
+    if mixed:
+        args.autocast_dtype = torch.bfloat16
+    model = RAFTStereo(args).eval().to(device)
+    g = torch.Generator().manual_seed(1234)
+    H, W = image_hw
+    img1 = (torch.rand(B, 3, H, W, generator=g) * 255).to(device)
+    img2 = torch.roll(img1, shifts=-8, dims=-1)
+    with torch.no_grad():
+        for _ in range(warmup):
+            model(img1, img2, iters=iters)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            model(img1, img2, iters=iters)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+    return {"pairs_per_s": B / dt, "ms_per_batch": dt * 1e3, "batch": B, "image": [H, W],
+            "iters": iters, "mixed_precision": mixed,
+            "note": "full network; encoders/GRU/heads on PyTorch (MIOpen) ops per north_star"}
+
+
 def load_traffic(path):
     try:
         with open(path) as fh:
@@ -136,6 +170,10 @@ def main():
     ap.add_argument("--config", default="sceneflow", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one step (build + lookups) in a HIP graph and replay it")
+    ap.add_argument("--e2e-steps", type=int, default=2,
+                    help="also time the whole network this many steps (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -151,7 +189,9 @@ def main():
 
     cfg = CONFIGS[args.config]
     B, D, H, W1, W2, L, r, iters, desc = cfg
-    f1, f2, coords = make_inputs(cfg, device, seed=1 + rank)
+    bf16 = args.config in BF16_CONFIGS
+    f1, f2, coords = make_inputs(cfg, device, seed=1 + rank,
+                                 dtype=torch.bfloat16 if bf16 else torch.float32)
     P = B * H * W1
 
     def step(ev=None):
@@ -166,9 +206,30 @@ def main():
             ev[2].record()
         return out
 
+    run = step
+    if args.graph:
+        # The whole step -- pyramid allocation (graph memory pool) and every
+        # libraftcorr launch on the capturing stream -- becomes one replay.
+        with torch.no_grad():
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+        torch.cuda.synchronize()
+
+        def run(ev=None):
+            if ev is not None:
+                ev[0].record()
+                ev[1].record()
+            graph.replay()
+            if ev is not None:
+                ev[2].record()
+
     with torch.no_grad():
         for _ in range(args.warmup):
-            step()
+            run()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -178,7 +239,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(args.steps):
-            step(evs[k])
+            run(evs[k])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -186,6 +247,14 @@ def main():
         build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
         lookup_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps / iters
 
+        if args.graph:   # a replay has no per-kernel events: time eager builds instead
+            be = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(5)]
+            for e0, e1 in be:
+                e0.record()
+                CorrBlock1D(f1, f2, num_levels=L, radius=r)
+                e1.record()
+            torch.cuda.synchronize()
+            build_ms = sum(e0.elapsed_time(e1) for e0, e1 in be) / len(be)
         # per-launch lookup duration without the host gaps between launches:
         # events around each launch of one extra pass
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
@@ -197,6 +266,16 @@ def main():
         torch.cuda.synchronize()
         lookup_launch_ms = sum(a.elapsed_time(b) for a, b in le) / iters
 
+    # per-step latency distribution (p50) for the latency-bound realtime config
+    lat = []
+    with torch.no_grad():
+        for _ in range(min(args.steps, 50)):
+            torch.cuda.synchronize()
+            a0 = time.perf_counter()
+            run()
+            torch.cuda.synchronize()
+            lat.append((time.perf_counter() - a0) * 1e3)
+    lat.sort()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -205,18 +284,27 @@ def main():
     value = world * B * args.steps / sec
 
     vflops = volume_flops(B, D, H, W1, W2)
-    lbytes = lookup_bytes(P, L, r)
+    s_el = 2 if bf16 else 4
+    lbytes = lookup_bytes(P, L, r, s_pyr=s_el)
+    vbytes = volume_bytes(B, D, H, W1, W2, L, s_in=s_el, s_pyr=s_el)
     traffic = load_traffic(args.traffic).get(args.config, {})
-    roof_volume = {"bound": "mfma", "achieved": vflops / (build_ms * 1e-3) / 1e12,
-                   "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                   "frac": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                   "traffic": traffic.get("build_bytes"),
-                   "algorithmic_bytes": volume_bytes(B, D, H, W1, W2, L),
-                   "kernel": "rc::build_f32_kernel", "avg_launch_us": build_ms * 1e3}
+    if bf16:   # HBM-bound in bf16: price the volume in bytes
+        vgbs = vbytes / (build_ms * 1e-3) / 1e9
+        roof_volume = {"bound": "hbm", "achieved": vgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": vgbs / HBM_PEAK_GBS, "traffic": traffic.get("build_bytes"),
+                       "algorithmic_bytes": vbytes, "flops": vflops,
+                       "kernel": "rc::build_bf16_kernel", "avg_launch_us": build_ms * 1e3}
+    else:
+        roof_volume = {"bound": "mfma", "achieved": vflops / (build_ms * 1e-3) / 1e12,
+                       "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                       "traffic": traffic.get("build_bytes"), "algorithmic_bytes": vbytes,
+                       "kernel": "rc::build_f32_kernel", "avg_launch_us": build_ms * 1e3}
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": lgbs / HBM_PEAK_GBS, "traffic": traffic.get("lookup_bytes"),
-                   "algorithmic_bytes": lbytes, "kernel": "rc::lookup_kernel<4,0,false,true>",
+                   "algorithmic_bytes": lbytes,
+                   "kernel": f"rc::lookup_kernel<{r},0,{'true' if bf16 else 'false'},true>",
                    "avg_launch_us": lookup_launch_ms * 1e3}
     dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
 
@@ -231,19 +319,25 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (randn fmaps, coords_grid - U[0,64) per iteration)",
-        "config": {"workload": desc, "config": args.config, "global_batch": B * world,
+        "config": {"workload": desc + (" (HIP graph replay)" if args.graph else ""),
+                   "config": args.config, "global_batch": B * world,
                    "fmap": [B, D, H, W1], "W2": W2, "levels": L, "radius": r, "iters": iters,
                    "parallelism": f"batch-shard x{world}"},
         "roofline": dominant,
         "roofline_volume": roof_volume,
         "roofline_lookup": roof_lookup,
         "lookup_gbs": lgbs,
+        "latency_ms": {"p50": lat[len(lat) // 2], "min": lat[0], "max": lat[-1]},
         "kernel_ms": {"build": build_ms, "lookup_in_loop": lookup_ms,
                       "lookup_per_launch": lookup_launch_ms},
         "cpu_baseline": None,
     }
+    if args.e2e_steps > 0 and args.config == "sceneflow":
+        result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1)
+        result["e2e"]["pairs_per_s_all_ranks"] = result["e2e"]["pairs_per_s"] * world
+        result["e2e"]["corr_path_share"] = (ms_per_step / result["e2e"]["ms_per_batch"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:

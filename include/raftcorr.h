@@ -53,7 +53,12 @@ const char *rc_last_error(void);
  *          of level l along w2 (floor width).  The reference builds
  *          num_levels+1 buffers (model.py:293); pass nbuf = num_levels + 1.
  *   Requires (W2 >> (nbuf-1)) >= 1 (the reference raises otherwise) and
- *   16-byte aligned pointers. */
+ *   16-byte aligned pointers.
+ *   Arithmetic: fmap_dtype == pyr_dtype == RC_F32 runs the exact fp32 MFMA
+ *   kernel (v_mfma_f32_16x16x4_f32).  Any bf16 operand (bf16 fmaps, or a
+ *   bf16 pyramid requested for fp32 fmaps, which are rounded to bf16 on
+ *   load) runs the bf16 MFMA kernel (v_mfma_f32_16x16x32_bf16, fp32
+ *   accumulation); pooling is done on the fp32 accumulators either way. */
 int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtype,
                   int B, int D, int H, int W1, int W2,
                   void *const *pyr, int nbuf, int pyr_dtype, void *stream);

@@ -20,9 +20,10 @@ RuntimeError (einsum, :324); coords that do not match the volume's
 RuntimeError (grid_sample dtype check, :275).
 
 Differences, all loud: tensors must live on a HIP device (no CPU fallback);
-the path is inference-only (asking for gradients raises); bf16 fmaps are
-accepted (the reference crashes on them) and an
-optional ``pyramid_dtype=torch.bfloat16`` stores the pyramid in bf16.
+the path is inference-only (asking for gradients raises); bf16/fp16 fmaps are
+accepted (the reference crashes on them): they, or
+an explicit ``pyramid_dtype=torch.bfloat16``, select the bf16 MFMA kernel and
+a bf16 pyramid (bf16-level tolerance).
 """
 import torch
 
@@ -75,11 +76,11 @@ def _check_fmaps(fmap1, fmap2):
 
 
 def _prep_fmap(f):
-    # fp32 MFMA path consumes fp32; bf16/fp16 fmaps (autocast) are widened
-    # here until the bf16 MFMA variant lands ("bf16").
-    if f.dtype in (torch.bfloat16, torch.float16):
+    # fp32 and bf16 go to the kernels as they are; fp16 (default autocast)
+    # is widened to fp32 and then rounded to bf16 on load by the bf16 kernel.
+    if f.dtype == torch.float16:
         f = f.float()
-    elif f.dtype != torch.float32:
+    elif f.dtype not in (torch.float32, torch.bfloat16):
         raise TypeError(f"raft_stereo_amd: unsupported fmap dtype {f.dtype}")
     return f.contiguous()
 
@@ -94,6 +95,8 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32):
     if nbuf > _lib.RC_MAX_LEVELS:
         raise RuntimeError(f"CorrBlock1D: at most {_lib.RC_MAX_LEVELS - 1} levels supported")
     f1, f2 = _prep_fmap(fmap1), _prep_fmap(fmap2)
+    if f1.dtype != f2.dtype:
+        f1, f2 = f1.float(), f2.float()
     P = B * H * W1
     pyr = [torch.empty((P, 1, 1, W2 >> l), dtype=pyramid_dtype, device=f1.device)
            for l in range(nbuf)]
@@ -101,7 +104,7 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32):
         return pyr
     with torch.cuda.device(f1.device):
         rc = _lib.lib().rc_corr_build(
-            f1.data_ptr(), f2.data_ptr(), _lib.RC_F32, B, D, H, W1, W2,
+            f1.data_ptr(), f2.data_ptr(), _dtype_code(f1.dtype), B, D, H, W1, W2,
             _lib.ptr_array([t.data_ptr() for t in pyr]), nbuf,
             _dtype_code(pyramid_dtype), _stream(f1.device))
     _lib.check(rc, "rc_corr_build")

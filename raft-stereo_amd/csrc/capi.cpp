@@ -57,8 +57,6 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
         return fail(RC_EINVAL, "rc_corr_build: unknown fmap dtype %d", fmap_dtype);
     if (pyr_dtype != RC_F32 && pyr_dtype != RC_BF16)
         return fail(RC_EINVAL, "rc_corr_build: unknown pyramid dtype %d", pyr_dtype);
-    if (fmap_dtype == RC_BF16)
-        return fail(RC_EUNSUPPORTED, "rc_corr_build: bf16 feature maps not built in this version");
     if (!pyr) return fail(RC_EINVAL, "rc_corr_build: null pyramid array");
     if ((long long)B * H * W1 == 0) return RC_OK;
     if (!fmap1 || !fmap2 || !aligned16(fmap1) || !aligned16(fmap2))
@@ -80,7 +78,12 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     a.scale = 1.0f / a.sq;                      // exact when pow2
     a.pyr_bf16 = pyr_dtype == RC_BF16;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    int rc = hip_rc(rc_launch_build_f32(a, s), "rc_corr_build: volume launch");
+    // fp32 fmaps + fp32 pyramid: exact fp32 MFMA.  bf16 fmaps, or a bf16
+    // pyramid (bf16-level tolerance requested), take the bf16 MFMA kernel.
+    const bool bf16_mma = fmap_dtype == RC_BF16 || pyr_dtype == RC_BF16;
+    int rc = hip_rc(bf16_mma ? rc_launch_build_bf16mma(a, fmap_dtype == RC_BF16, s)
+                             : rc_launch_build_f32(a, s),
+                    "rc_corr_build: volume launch");
     if (rc) return rc;
     const long rows = (long)B * H * W1;
     for (int l = a.nfused; l < nbuf; ++l) {

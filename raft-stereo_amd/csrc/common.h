@@ -67,6 +67,7 @@ struct LookupArgs {
 
 // Host-side launchers (defined in the .hip files, called by capi.cpp).
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s);
+hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStream_t s);
 hipError_t rc_launch_pool(const void *in, void *out, long rows, int W_in, int bf16,
                           hipStream_t s);
 hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s);

@@ -166,38 +166,16 @@ __device__ __forceinline__ void mma_stage(const Stage<FM, U> &s, f32x4 (&acc)[FM
                                                                    acc[ma][nb], 0, 0, 0);
 }
 
-template <int FM, int U, bool VEC, int MODE>
-__device__ __forceinline__ void wave_tile(const BuildArgs &a, int row, int b, int h, int m0,
-                                          int n0, int lane, float *stA, float *stB) {
-    const int D = a.D, H = a.H, W1 = a.W1, W2 = a.W2;
-    const long long img1 = (long long)D * H * W1, img2 = (long long)D * H * W2;
-    const auto r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
-    const auto r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
-    const int kd = lane >> 4;             // d offset inside a k-step
-    const int wa = m0 + FM * (lane & 15); // this lane's w1 group
+// Epilogue shared by the fp32 and bf16 kernels: scale, level 0 from
+// registers, pooled levels through the wave's LDS staging image.
+// acc[ma][nb] register r of lane l holds C[m0 + R][n0 + 4*(l&15) + nb] with
+// R = FM*((l>>4)*4 + r) + ma (interleaved rows, fp32 kernel) or
+// R = 16*ma + (l>>4)*4 + r (blocked rows, bf16 kernel).
+template <int FM, int MODE, bool BLOCKED, bool VEC>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildArgs &a, int row,
+                                         int m0, int n0, int lane, float *stA, float *stB) {
+    const int W1 = a.W1, W2 = a.W2;
     const int wb = n0 + 4 * (lane & 15);  // this lane's w2 quad
-
-    f32x4 acc[FM][4];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    constexpr int KS = 4 * U;                      // d per stage
-    const int nst = (D + KS - 1) / KS;             // stages (tail stages read zeros)
-    Stage<FM, U> s0, s1;
-    load_stage<FM, U, VEC, MODE>(s0, 0, kd, r1, r2, D, H, h, W1, W2, wa, wb);
-    load_stage<FM, U, VEC, MODE>(s1, KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
-    for (int st = 0; st < nst; st += 2) {
-        mma_stage<FM, U>(s0, acc);
-        if (st + 2 < nst) load_stage<FM, U, VEC, MODE>(s0, (st + 2) * KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
-        if (st + 1 < nst) {
-            mma_stage<FM, U>(s1, acc);
-            if (st + 3 < nst) load_stage<FM, U, VEC, MODE>(s1, (st + 3) * KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
-        }
-    }
-
-    // ---- epilogue: scale, level 0, fused pooling (model.py:294) ----
     const long long rowbase = (long long)row * W1;  // pyramid row of w1 = 0
     const int col = lane & 15;
     const bool bf = a.pyr_bf16 != 0;
@@ -206,7 +184,8 @@ __device__ __forceinline__ void wave_tile(const BuildArgs &a, int row, int b, in
     for (int ma = 0; ma < FM; ++ma) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int R = FM * ((lane >> 4) * 4 + r) + ma;  // tile row (w1 - m0)
+            const int R = BLOCKED ? 16 * ma + (lane >> 4) * 4 + r
+                              : FM * ((lane >> 4) * 4 + r) + ma;  // tile row (w1 - m0)
             const int w1 = m0 + R;
             const bool rv = w1 < W1;
             const long long p = rowbase + w1;
@@ -288,6 +267,41 @@ __device__ __forceinline__ void wave_tile(const BuildArgs &a, int row, int b, in
     }
 }
 
+
+template <int FM, int U, bool VEC, int MODE>
+__device__ __forceinline__ void wave_tile(const BuildArgs &a, int row, int b, int h, int m0,
+                                          int n0, int lane, float *stA, float *stB) {
+    const int D = a.D, H = a.H, W1 = a.W1, W2 = a.W2;
+    const long long img1 = (long long)D * H * W1, img2 = (long long)D * H * W2;
+    const auto r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
+    const auto r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
+    const int kd = lane >> 4;             // d offset inside a k-step
+    const int wa = m0 + FM * (lane & 15); // this lane's w1 group
+    const int wb = n0 + 4 * (lane & 15);  // this lane's w2 quad
+
+    f32x4 acc[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int KS = 4 * U;                      // d per stage
+    const int nst = (D + KS - 1) / KS;             // stages (tail stages read zeros)
+    Stage<FM, U> s0, s1;
+    load_stage<FM, U, VEC, MODE>(s0, 0, kd, r1, r2, D, H, h, W1, W2, wa, wb);
+    load_stage<FM, U, VEC, MODE>(s1, KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
+    for (int st = 0; st < nst; st += 2) {
+        mma_stage<FM, U>(s0, acc);
+        if (st + 2 < nst) load_stage<FM, U, VEC, MODE>(s0, (st + 2) * KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
+        if (st + 1 < nst) {
+            mma_stage<FM, U>(s1, acc);
+            if (st + 3 < nst) load_stage<FM, U, VEC, MODE>(s1, (st + 3) * KS, kd, r1, r2, D, H, h, W1, W2, wa, wb);
+        }
+    }
+
+    epilogue<FM, MODE, false, VEC>(acc, a, row, m0, n0, lane, stA, stB);
+}
+
 template <bool VEC, int U, int MODE>
 __global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a, int nwg_total) {
     // one LDS array (guide §5 trap 4a): per wave an 8 KB + 4 KB ping-pong
@@ -319,12 +333,219 @@ __global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a, int nwg_tot
     tile_body(blockIdx.x);
 }
 
+// ===================== bf16 MFMA path (HBM-bound) =====================
+//
+// v_mfma_f32_16x16x32_bf16: lane l supplies A[i=l&15][k=8(l>>4)+j] and
+// B[k=8(l>>4)+j][j'=l&15], j = 0..7 -- eight consecutive k (= d) per lane,
+// while the NCHW fmaps are contiguous along w.  Each wave therefore stages
+// its [32 d][64 w] operand tiles in a private LDS image (rows padded to
+// 160 B: conflict-free for both the row writes and the transposed reads) and
+// reads fragments with ds_read_b64_tr_b16, which hands lane i column i of a
+// 4-row block.  A's image is in natural w order (fragment ma = 16 consecutive
+// w1); B's columns are permuted, column 16*nb + i <- w2 = n0 + 4i + nb, so the
+// accumulator layout is the fp32 kernel's (4 consecutive w2 per lane) and the
+// same epilogue applies with blocked rows.  The LDS image is private to the
+// wave: LDS executes a wave's instructions in order, so no barriers.
+// Rows whose start is not 16-B aligned (e.g. W = 311) load two aligned chunks
+// and shift in registers.
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kImgRow = 160;              // bytes per LDS image row (64 bf16 + pad)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// One 16x16x32 operand fragment: two transposed 4-row reads (d = 8g+q and
+// 8g+4+q rows of the image, this lane's 4 columns), i.e. k = 8g .. 8g+7.
+__device__ __forceinline__ bf16x8 read_frag(const char *p) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p + 4 * kImgRow));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+constexpr int kImgBytes = 32 * kImgRow;   // one operand image
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+    return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+}
+
+// 8 consecutive elements (as 4 dwords of bf16 pairs) starting at element
+// index e of one image; zeros when off-range (d >= D pushes e out of range).
+template <bool IN_BF16, bool ALIGNED>
+__device__ __forceinline__ u32x4 load_chunk8(__amdgpu_buffer_rsrc_t r, long long e, bool valid) {
+    if constexpr (IN_BF16) {
+        if constexpr (ALIGNED) {
+            const uint32_t off = valid ? (uint32_t)(e * 2) : 0xFFFFFF00u;
+            return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+        } else {
+            const long long ea = e & ~7LL;
+            const int sft = (int)(e - ea);                 // 0..7 elements
+            const uint32_t off = valid ? (uint32_t)(ea * 2) : 0xFFFFFF00u;
+            const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+            const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off + 16u), 0, 0);
+            const unsigned x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            const int dsh = sft >> 1;
+            u32x4 out;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                unsigned a0 = x[k], a1 = x[k + 1];
+#pragma unroll
+                for (int t = 1; t < 4; ++t) {
+                    a0 = (dsh == t) ? x[k + t] : a0;
+                    a1 = (dsh == t) ? x[k + t + 1] : a1;
+                }
+                out[k] = (sft & 1) ? __builtin_amdgcn_alignbyte(a1, a0, 2) : a0;
+            }
+            return out;
+        }
+    } else {
+        float v[8];
+        if constexpr (ALIGNED) {
+            const uint32_t off = valid ? (uint32_t)(e * 4) : 0xFFFFFF00u;
+            const f32x4 p0 = ld4(r, off), p1 = ld4(r, off + 16u);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) { v[c] = p0[c]; v[4 + c] = p1[c]; }
+        } else {
+            const long long ea = e & ~3LL;
+            const int sft = (int)(e - ea);                 // 0..3 elements
+            const uint32_t off = valid ? (uint32_t)(ea * 4) : 0xFFFFFF00u;
+            float x[12];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const f32x4 p = ld4(r, off + 16u * q);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) x[4 * q + c] = p[c];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                float t = x[k];
+#pragma unroll
+                for (int u = 1; u < 4; ++u) t = (sft == u) ? x[k + u] : t;
+                v[k] = t;
+            }
+        }
+        u32x4 out;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
+        return out;
+    }
+}
+
+template <bool IN_BF16, bool ALIGNED, int MODE>
+__device__ __forceinline__ void wave_tile_bf16(const BuildArgs &a, int row, int b, int h, int m0,
+                                               int n0, int lane, char *img, float *stA, float *stB) {
+    const int D = a.D, H = a.H, W1 = a.W1, W2 = a.W2;
+    constexpr int ES = IN_BF16 ? 2 : 4;
+    const long long img1 = (long long)D * H * W1, img2 = (long long)D * H * W2;
+    const auto r1 = make_rsrc(reinterpret_cast<const char *>(a.f1) + b * img1 * ES, clamp_bytes(img1 * ES));
+    const auto r2 = make_rsrc(reinterpret_cast<const char *>(a.f2) + b * img2 * ES, clamp_bytes(img2 * ES));
+    char *imgA = img, *imgB = img + kImgBytes;
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // staging assignment: chunk c = lane + 64t (t = 0..3) -> d-row c>>3, w chunk c&7
+    u32x4 ra[4], rb[4];
+    auto load_step = [&](int k0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int c = lane + 64 * t, d = k0 + (c >> 3), m = c & 7;
+            const bool ok = d < D;
+            const long long base = (long long)(ok ? d : 0) * H + h;
+            ra[t] = load_chunk8<IN_BF16, ALIGNED>(r1, base * W1 + m0 + 8 * m, ok);
+            rb[t] = load_chunk8<IN_BF16, ALIGNED>(r2, base * W2 + n0 + 8 * m, ok);
+        }
+    };
+    auto write_step = [&]() {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int c = lane + 64 * t, dr = c >> 3, m = c & 7;
+            *reinterpret_cast<u32x4 *>(imgA + dr * kImgRow + 16 * m) = ra[t];
+            // B: element e of the chunk (w2 = n0 + 8m + e) goes to column
+            // 16*(e&3) + 2m + (e>>2); elements e and e+4 share one dword.
+            const u32x4 u = rb[t];
+            const unsigned pk[4] = {(u[0] & 0xFFFFu) | (u[2] << 16), (u[0] >> 16) | (u[2] & 0xFFFF0000u),
+                                    (u[1] & 0xFFFFu) | (u[3] << 16), (u[1] >> 16) | (u[3] & 0xFFFF0000u)};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                *reinterpret_cast<unsigned *>(imgB + dr * kImgRow + 32 * k + 4 * m) = pk[k];
+        }
+    };
+    // transposed-read address of this lane inside a 4-row x 16-col block
+    const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, p4 = lane & 3;
+
+    const int nk = (D + 31) >> 5;
+    load_step(0);
+    for (int ks = 0; ks < nk; ++ks) {
+        write_step();
+        if (ks + 1 < nk) load_step((ks + 1) * 32);
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int colb = (16 * f + 4 * p4) * 2;
+            fa[f] = read_frag(imgA + (8 * g + q) * kImgRow + colb);
+            fb[f] = read_frag(imgB + (8 * g + q) * kImgRow + colb);
+        }
+#pragma unroll
+        for (int ma = 0; ma < 4; ++ma)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+                acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ma], fb[nb], acc[ma][nb], 0, 0, 0);
+    }
+    epilogue<4, MODE, true, ALIGNED>(acc, a, row, m0, n0, lane, stA, stB);
+}
+
+template <bool IN_BF16, bool ALIGNED, int MODE>
+__global__ __launch_bounds__(256) void build_bf16_kernel(BuildArgs a, int nwg_total) {
+    // per wave: 2 operand images (10 KB) during the K loop, then the 12 KB
+    // epilogue staging area (aliases them: the loop is over by then)
+    __shared__ __attribute__((aligned(16))) float smem[4][kStageFloats + kStageFloats / 2];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *stA = smem[wave], *stB = smem[wave] + kStageFloats;
+    char *img = reinterpret_cast<char *>(smem[wave]);
+    const int T = a.tiles_m * a.tiles_n;
+    const int v = blockIdx.x;
+    const int xcd = v & 7, q = nwg_total >> 3, rr = nwg_total & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (v >> 3);
+    const int row = wgid / T, tile = wgid - row * T;
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int b = row / a.H, h = row - b * a.H;
+    const int m0 = tm * 128 + (wave >> 1) * 64;
+    const int n0 = tn * 128 + (wave & 1) * 64;
+    if (m0 >= a.W1 || n0 >= a.W2) return;   // wave-uniform; no barriers in this kernel
+    wave_tile_bf16<IN_BF16, ALIGNED, MODE>(a, row, b, h, m0, n0, lane, img, stA, stB);
+}
+
 template <bool VEC, int U, int MODE>
 static void launch(const BuildArgs &a, unsigned nwg, hipStream_t s) {
     hipLaunchKernelGGL((build_f32_kernel<VEC, U, MODE>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
 }
 
+template <bool IN_BF16, bool ALIGNED>
+static void launch_bf16(const BuildArgs &a, unsigned nwg, hipStream_t s) {
+    hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 0>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
+}
+
 }  // namespace rc
+
+hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStream_t s) {
+    const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
+    if (nwg <= 0) return hipSuccess;
+    if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
+    const unsigned n = (unsigned)nwg;
+    if (in_bf16) {
+        if (a.W1 % 8 == 0 && a.W2 % 8 == 0) rc::launch_bf16<true, true>(a, n, s);
+        else rc::launch_bf16<true, false>(a, n, s);
+    } else {
+        if (a.W1 % 4 == 0 && a.W2 % 4 == 0) rc::launch_bf16<false, true>(a, n, s);
+        else rc::launch_bf16<false, false>(a, n, s);
+    }
+    return hipGetLastError();
+}
 
 // RAFTCORR_BUILD_MODE (dev-only ablation, read per call): flags 1 no operand
 // loads, 2 no epilogue stores, 4 prefetch U=4 (default U=2), 8 register

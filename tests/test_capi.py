@@ -51,7 +51,6 @@ def _build(**kw):
     (dict(D=0), _lib.RC_EINVAL),
     (dict(dt=7), _lib.RC_EINVAL),
     (dict(pdt=5), _lib.RC_EINVAL),
-    (dict(dt=1), _lib.RC_EUNSUPPORTED),
     (dict(), _lib.RC_EINVAL),                   # null feature maps
 ])
 def test_build_validation(kw, code):

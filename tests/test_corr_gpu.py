@@ -163,3 +163,44 @@ def test_repeat_launches_deterministic():
         outs = [CorrBlock1D(f1, f2)(c) for _ in range(5)]
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
+
+
+BF16_SHAPES = [
+    (1, 256, 2, 64, 64, 4, 4),
+    (2, 256, 2, 311, 311, 4, 4),    # config-3 width: rows not 16-B aligned
+    (1, 96, 3, 40, 57, 3, 3),       # D % 32 != 0, odd W2
+    (1, 37, 2, 24, 33, 4, 2),
+]
+
+
+@pytest.mark.parametrize("shape", BF16_SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("mode", ["bf16in_f32pyr", "bf16in_bf16pyr", "f32in_bf16pyr"])
+def test_bf16_mma_vs_oracle(shape, mode):
+    """bf16 MFMA kernel vs the fp64-accumulated oracle on bf16-rounded inputs.
+    Tolerances: fp32 pyramid 1e-5 normalised (only the summation order
+    differs: bf16 products are exact in fp32); bf16 pyramid 8e-3 normalised
+    (one bf16 rounding of each stored value)."""
+    B, D, H, W1, W2, L, r = shape
+    g = torch.Generator().manual_seed(7 + sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    f1r, f2r = f1.bfloat16().float(), f2.bfloat16().float()   # what the kernel multiplies
+    x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 40
+    coords = torch.cat([x, torch.zeros_like(x)], 1)
+    in_dt = torch.float32 if mode.startswith("f32in") else torch.bfloat16
+    pyr_dt = torch.bfloat16 if mode.endswith("bf16pyr") else torch.float32
+    with torch.no_grad():
+        blk = CorrBlock1D(f1.to(DEV, in_dt), f2.to(DEV, in_dt), num_levels=L, radius=r,
+                          pyramid_dtype=pyr_dt)
+        out = blk(coords.to(DEV)).cpu().numpy()
+    assert blk.corr_pyramid[0].dtype == pyr_dt
+    got = pyr_np(blk)
+    ref = coracle.corr_pyramid(f1r.numpy(), f2r.numpy(), L)
+    tol = 1e-5 if pyr_dt == torch.float32 else 8e-3
+    for i in range(L + 1):
+        assert norm_err(got[i], ref[i]) <= tol, f"level {i}"
+    if pyr_dt == torch.float32:
+        for i in range(L):
+            assert same(got[i + 1], coracle.corr_pool(got[i]))
+    # the lookup reads the stored (bf16 or fp32) pyramid exactly
+    assert same(out, coracle.corr_lookup(got[:L], coords.numpy(), L, r))
