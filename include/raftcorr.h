@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 1
+#define RC_ABI_VERSION 2
 
 /* element types */
 #define RC_F32  0
@@ -48,10 +48,14 @@ const char *rc_last_error(void);
 /* Volume + pyramid (model.py:284-295, :318-326).
  *   fmap1: [B][D][H][W1], fmap2: [B][D][H][W2], contiguous, element type
  *          fmap_dtype (RC_F32, or RC_BF16 for the bf16 MFMA path).
- *   pyr[l], l < nbuf: device buffers [B*H*W1][W2 >> l] of pyr_dtype; level 0
- *          is the volume divided by sqrtf(D), level l+1 is the pairwise mean
- *          of level l along w2 (floor width).  The reference builds
- *          num_levels+1 buffers (model.py:293); pass nbuf = num_levels + 1.
+ *   pyr[l], l < nbuf: device buffers of B*H*W1 rows of W2 >> l elements of
+ *          pyr_dtype, row stride pyr_ld[l] elements (>= W2 >> l; NULL pyr_ld =
+ *          dense rows).  Level 0 is the volume divided by sqrtf(D), level l+1
+ *          the pairwise mean of level l along w2 (floor width).  The
+ *          reference builds num_levels+1 buffers (model.py:293); pass
+ *          nbuf = num_levels + 1.  Padding rows to a multiple of 16 bytes lets
+ *          every store be a full aligned vector (the padding is written with
+ *          don't-care values and never read).
  *   Requires (W2 >> (nbuf-1)) >= 1 (the reference raises otherwise) and
  *   16-byte aligned pointers.
  *   Arithmetic: fmap_dtype == pyr_dtype == RC_F32 runs the exact fp32 MFMA
@@ -61,22 +65,25 @@ const char *rc_last_error(void);
  *   accumulation); pooling is done on the fp32 accumulators either way. */
 int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtype,
                   int B, int D, int H, int W1, int W2,
-                  void *const *pyr, int nbuf, int pyr_dtype, void *stream);
+                  void *const *pyr, const long *pyr_ld, int nbuf, int pyr_dtype,
+                  void *stream);
 
 /* One pooling step (model.py:294): out[p][j] = (in[p][2j] + in[p][2j+1]) / 2,
- * j < W_in/2, for p < rows.  dtype RC_F32 or RC_BF16 (bf16 rounds once). */
-int rc_corr_pool(const void *in, void *out, long rows, int W_in, int dtype,
-                 void *stream);
+ * j < W_in/2, for p < rows; row strides ld_in / ld_out elements.  dtype
+ * RC_F32 or RC_BF16 (bf16 rounds once). */
+int rc_corr_pool(const void *in, long ld_in, void *out, long ld_out, long rows,
+                 int W_in, int dtype, void *stream);
 
 /* Lookup (model.py:297-316, :267-281).
- *   pyr[i], i < levels: [B*H*W1][widths[i]] of pyr_dtype (16-byte aligned).
+ *   pyr[i], i < levels: B*H*W1 rows of widths[i] elements of pyr_dtype, row
+ *          stride pyr_ld[i] elements (NULL = dense), 16-byte aligned base.
  *   coords_x: x channel of the (B,2,H,W1) fp32 coords, element (b,h,w) at
  *          coords_x[b*coord_batch_stride + h*W1 + w] (the y channel is
  *          ignored, model.py:299/:308).
  *   out:   [B][levels*(2*radius+1)][H][W1] fp32, channel = level*(2r+1)+(t+r).
  *   radius in 1..8, levels in 1..RC_MAX_LEVELS. */
-int rc_corr_lookup(const void *const *pyr, const int *widths, int pyr_dtype,
-                   int levels, int radius, const float *coords_x,
+int rc_corr_lookup(const void *const *pyr, const int *widths, const long *pyr_ld,
+                   int pyr_dtype, int levels, int radius, const float *coords_x,
                    long coord_batch_stride, int B, int H, int W1, float *out,
                    void *stream);
 

@@ -14,7 +14,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 RC_F32, RC_BF16 = 0, 1
 RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # name -> (restype, argtypes); must match include/raftcorr.h exactly.
 _vp, _i, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
@@ -22,10 +22,10 @@ SIGNATURES = {
     "rc_abi_version": (_i, []),
     "rc_last_error": (ctypes.c_char_p, []),
     "rc_corr_build": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i,
-                           ctypes.POINTER(_vp), _i, _i, _vp]),
-    "rc_corr_pool": (_i, [_vp, _vp, _l, _i, _i, _vp]),
-    "rc_corr_lookup": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), _i, _i, _i,
-                            _vp, _l, _i, _i, _i, _vp, _vp]),
+                           ctypes.POINTER(_vp), ctypes.POINTER(_l), _i, _i, _vp]),
+    "rc_corr_pool": (_i, [_vp, _l, _vp, _l, _l, _i, _i, _vp]),
+    "rc_corr_lookup": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i, _i,
+                            _i, _vp, _l, _i, _i, _i, _vp, _vp]),
 }
 
 _lib = None
@@ -68,3 +68,7 @@ def ptr_array(ptrs):
 
 def int_array(vals):
     return (ctypes.c_int * len(vals))(*vals)
+
+
+def long_array(vals):
+    return (ctypes.c_long * len(vals))(*vals)

@@ -8,7 +8,9 @@ so that ``RAFTStereo.forward`` can bind it where the reference does
       builds the all-pairs per-row volume / sqrt(D) and its avg-pooled
       pyramid in ONE kernel launch (rc_corr_build).  ``corr_pyramid`` holds
       num_levels+1 tensors of shape (B*H*W1, 1, 1, W2 >> l) like the reference
-      (:290-295); the last one is never read, as in the reference.
+      (:290-295; the last one is never read, as in the reference).  Rows whose
+      width is not a 16-byte multiple are views into row-padded buffers
+      (same shape and values, a larger row stride).
   * ``__call__(coords)``  (model.py:297-316)  one rc_corr_lookup launch:
       (B,2,H,W1) fp32 coords -> (B, num_levels*(2r+1), H, W1) fp32.
   * ``CorrBlock1D.corr(fmap1, fmap2)``  (model.py:318-326) -> (B,H,W1,1,W2).
@@ -85,8 +87,28 @@ def _prep_fmap(f):
     return f.contiguous()
 
 
-def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32):
-    """Run rc_corr_build: returns ``nbuf`` tensors (B*H*W1, 1, 1, W2 >> l)."""
+def _level_buffer(P, W, dtype, device, pad):
+    """(P, 1, 1, W) tensor whose rows start 16-byte aligned: a view of a
+    (P, ld) buffer with ld = W rounded up to 16 bytes when ``pad`` (the
+    kernels then store whole aligned vectors; the padding is never read)."""
+    per16 = 16 // torch.tensor([], dtype=dtype).element_size()
+    ld = -(-W // per16) * per16 if pad else W
+    buf = torch.empty((P, ld), dtype=dtype, device=device)
+    if ld == W:
+        return buf.view(P, 1, 1, W)
+    return buf[:, :W].unsqueeze(1).unsqueeze(1)
+
+
+def _row_stride(t):
+    """Row stride (elements) of a (P, 1, 1, W) level; rows must be unit-stride."""
+    if t.stride(-1) != 1:
+        raise RuntimeError("raft_stereo_amd: pyramid rows must be contiguous")
+    return t.stride(0) if t.shape[0] > 1 else t.shape[-1]
+
+
+def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True):
+    """Run rc_corr_build: returns ``nbuf`` tensors (B*H*W1, 1, 1, W2 >> l)
+    (row-padded views when ``pad``; values identical either way)."""
     B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
     if (W2 >> (nbuf - 1)) < 1:
         raise RuntimeError(
@@ -98,14 +120,14 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32):
     if f1.dtype != f2.dtype:
         f1, f2 = f1.float(), f2.float()
     P = B * H * W1
-    pyr = [torch.empty((P, 1, 1, W2 >> l), dtype=pyramid_dtype, device=f1.device)
-           for l in range(nbuf)]
+    pyr = [_level_buffer(P, W2 >> l, pyramid_dtype, f1.device, pad) for l in range(nbuf)]
     if P == 0:
         return pyr
     with torch.cuda.device(f1.device):
         rc = _lib.lib().rc_corr_build(
             f1.data_ptr(), f2.data_ptr(), _dtype_code(f1.dtype), B, D, H, W1, W2,
-            _lib.ptr_array([t.data_ptr() for t in pyr]), nbuf,
+            _lib.ptr_array([t.data_ptr() for t in pyr]),
+            _lib.long_array([_row_stride(t) for t in pyr]), nbuf,
             _dtype_code(pyramid_dtype), _stream(f1.device))
     _lib.check(rc, "rc_corr_build")
     return pyr
@@ -137,11 +159,13 @@ def lookup(pyramid, coords, num_levels, radius):
     if P == 0:
         return out
     levels = [pyramid[i] for i in range(num_levels)]
+    levels = [t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous() for t in levels]
     dt = levels[0].dtype
     with torch.cuda.device(coords.device):
         rc = _lib.lib().rc_corr_lookup(
             _lib.ptr_array([t.data_ptr() for t in levels]),
             _lib.int_array([t.shape[-1] for t in levels]),
+            _lib.long_array([_row_stride(t) for t in levels]),
             _dtype_code(dt), num_levels, radius, x.data_ptr(), cbs, B, H, W1,
             out.data_ptr(), _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup")
@@ -166,7 +190,7 @@ class CorrBlock1D:
     @staticmethod
     def corr(fmap1, fmap2):
         B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
-        lvl0 = build_pyramid(fmap1, fmap2, 1)[0]
+        lvl0 = build_pyramid(fmap1, fmap2, 1, pad=False)[0]
         return lvl0.view(B, H, W1, 1, W2)
 
 

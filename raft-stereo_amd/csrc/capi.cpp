@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/raftcorr.h"
 #include "common.h"
@@ -41,8 +42,8 @@ extern "C" int rc_abi_version(void) { return RC_ABI_VERSION; }
 extern "C" const char *rc_last_error(void) { return g_err; }
 
 extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtype, int B, int D,
-                             int H, int W1, int W2, void *const *pyr, int nbuf, int pyr_dtype,
-                             void *stream) {
+                             int H, int W1, int W2, void *const *pyr, const long *pyr_ld, int nbuf,
+                             int pyr_dtype, void *stream) {
     g_err[0] = 0;
     if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
         return fail(RC_EINVAL, "rc_corr_build: bad shape B=%d D=%d H=%d W1=%d W2=%d", B, D, H, W1, W2);
@@ -61,22 +62,30 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     if ((long long)B * H * W1 == 0) return RC_OK;
     if (!fmap1 || !fmap2 || !aligned16(fmap1) || !aligned16(fmap2))
         return fail(RC_EINVAL, "rc_corr_build: feature maps must be non-null and 16-byte aligned");
-    for (int l = 0; l < nbuf; ++l)
+    for (int l = 0; l < nbuf; ++l) {
         if (!pyr[l] || !aligned16(pyr[l]))
             return fail(RC_EINVAL, "rc_corr_build: pyramid buffer %d null or not 16-byte aligned", l);
+        if (pyr_ld && pyr_ld[l] < (long)(W2 >> l))
+            return fail(RC_EINVAL, "rc_corr_build: row stride %ld of level %d < width %d", pyr_ld[l],
+                        l, W2 >> l);
+    }
 
     rc::BuildArgs a{};
     a.f1 = fmap1;
     a.f2 = fmap2;
     a.B = B; a.D = D; a.H = H; a.W1 = W1; a.W2 = W2;
     a.nfused = nbuf < 7 ? nbuf : 7;
-    for (int l = 0; l < a.nfused; ++l) a.lvl[l] = pyr[l];
+    for (int l = 0; l < a.nfused; ++l) {
+        a.lvl[l] = pyr[l];
+        a.ld[l] = pyr_ld ? pyr_ld[l] : (W2 >> l);
+    }
     a.tiles_m = (W1 + 127) / 128;
     a.tiles_n = (W2 + 127) / 128;
     a.sq = std::sqrt((float)D);                 // torch.sqrt(torch.tensor(D).float()), :326
     a.pow2 = is_pow2_float(a.sq) ? 1 : 0;
     a.scale = 1.0f / a.sq;                      // exact when pow2
     a.pyr_bf16 = pyr_dtype == RC_BF16;
+    if (const char *e = getenv("RAFTCORR_STAGGER")) a.stagger = atoi(e);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // fp32 fmaps + fp32 pyramid: exact fp32 MFMA.  bf16 fmaps, or a bf16
     // pyramid (bf16-level tolerance requested), take the bf16 MFMA kernel.
@@ -87,30 +96,34 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     if (rc) return rc;
     const long rows = (long)B * H * W1;
     for (int l = a.nfused; l < nbuf; ++l) {
-        rc = hip_rc(rc_launch_pool(pyr[l - 1], pyr[l], rows, W2 >> (l - 1), a.pyr_bf16, s),
+        const long long ldi = pyr_ld ? pyr_ld[l - 1] : (W2 >> (l - 1));
+        const long long ldo = pyr_ld ? pyr_ld[l] : (W2 >> l);
+        rc = hip_rc(rc_launch_pool(pyr[l - 1], ldi, pyr[l], ldo, rows, W2 >> (l - 1), a.pyr_bf16, s),
                     "rc_corr_build: pool launch");
         if (rc) return rc;
     }
     return RC_OK;
 }
 
-extern "C" int rc_corr_pool(const void *in, void *out, long rows, int W_in, int dtype,
-                            void *stream) {
+extern "C" int rc_corr_pool(const void *in, long ld_in, void *out, long ld_out, long rows,
+                            int W_in, int dtype, void *stream) {
     g_err[0] = 0;
-    if (rows < 0 || W_in < 2)
-        return fail(RC_EINVAL, "rc_corr_pool: bad shape rows=%ld W_in=%d", rows, W_in);
+    if (rows < 0 || W_in < 2 || ld_in < W_in || ld_out < W_in / 2)
+        return fail(RC_EINVAL, "rc_corr_pool: bad shape rows=%ld W_in=%d ld_in=%ld ld_out=%ld", rows,
+                    W_in, ld_in, ld_out);
     if (dtype != RC_F32 && dtype != RC_BF16)
         return fail(RC_EINVAL, "rc_corr_pool: unknown dtype %d", dtype);
     if (rows == 0) return RC_OK;
     if (!in || !out) return fail(RC_EINVAL, "rc_corr_pool: null pointer");
-    return hip_rc(rc_launch_pool(in, out, rows, W_in, dtype == RC_BF16,
+    return hip_rc(rc_launch_pool(in, ld_in, out, ld_out, rows, W_in, dtype == RC_BF16,
                                  reinterpret_cast<hipStream_t>(stream)),
                   "rc_corr_pool: launch");
 }
 
-extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, int pyr_dtype, int levels,
-                              int radius, const float *coords_x, long coord_batch_stride, int B,
-                              int H, int W1, float *out, void *stream) {
+extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, const long *pyr_ld,
+                              int pyr_dtype, int levels, int radius, const float *coords_x,
+                              long coord_batch_stride, int B, int H, int W1, float *out,
+                              void *stream) {
     g_err[0] = 0;
     if (levels < 1 || levels > RC_MAX_LEVELS)
         return fail(RC_EINVAL, "rc_corr_lookup: levels=%d outside 1..%d", levels, RC_MAX_LEVELS);
@@ -133,6 +146,10 @@ extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, int pyr
             return fail(RC_EINVAL, "rc_corr_lookup: level %d null or not 16-byte aligned", i);
         a.lvl[i] = pyr[i];
         a.W[i] = widths[i];
+        a.ld[i] = pyr_ld ? pyr_ld[i] : widths[i];
+        if (a.ld[i] < widths[i])
+            return fail(RC_EINVAL, "rc_corr_lookup: level %d row stride %lld < width %d", i, a.ld[i],
+                        widths[i]);
     }
     a.coords = coords_x;
     a.cbs = coord_batch_stride;

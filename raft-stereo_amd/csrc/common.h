@@ -43,6 +43,7 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 struct BuildArgs {
     const void *f1, *f2;      // [B][D][H][W1], [B][D][H][W2]
     void *lvl[kMaxLevels];    // pyramid outputs
+    long long ld[kMaxLevels]; // their row strides (elements, >= W2 >> l)
     int B, D, H, W1, W2;
     int nfused;               // levels written by the epilogue (1..7)
     int tiles_m, tiles_n;     // 128x128 workgroup tiles per (b,h) row
@@ -50,11 +51,13 @@ struct BuildArgs {
     float sq;                 // sqrtf(D)
     int pow2;                 // sqrt(D) is a power of two -> multiply is exact
     int pyr_bf16;             // store pyramid as bf16
+    int stagger;              // dev-only: first-round stagger unit (s_sleep(127) count)
 };
 
 struct LookupArgs {
     const void *lvl[kMaxLevels];
     int W[kMaxLevels];
+    long long ld[kMaxLevels]; // row strides (elements, >= W)
     const float *coords;
     long long cbs;            // coords batch stride (elements)
     float *out;
@@ -68,6 +71,6 @@ struct LookupArgs {
 // Host-side launchers (defined in the .hip files, called by capi.cpp).
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s);
 hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStream_t s);
-hipError_t rc_launch_pool(const void *in, void *out, long rows, int W_in, int bf16,
-                          hipStream_t s);
+hipError_t rc_launch_pool(const void *in, long long ld_in, void *out, long long ld_out, long rows,
+                          int W_in, int bf16, hipStream_t s);
 hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s);

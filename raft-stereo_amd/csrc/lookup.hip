@@ -51,6 +51,7 @@ __device__ __forceinline__ void issue_level(LevelWindow<R, BF16> &lw, const Look
                                             float x, long long pblk, long long lrow) {
     typedef LevelWindow<R, BF16> LW;
     const int W = a.W[i];
+    const long long ld = a.ld[i];
     const float Wm1 = (float)(W - 1);
     const float half = Wm1 / 2.0f;
     const float xl = x / (float)(1 << i);
@@ -62,17 +63,17 @@ __device__ __forceinline__ void issue_level(LevelWindow<R, BF16> &lw, const Look
     }
     lw.inwin = (xl > -(float)(R + 4)) && (xl < (float)(W + R + 4));  // false for NaN
     lw.n = lw.inwin ? floorf(xl) : 0.0f;
-    const long long e = lrow * W + (long long)lw.n - (R + 1);
+    const long long e = lrow * ld + (long long)lw.n - (R + 1);
     const long long ea = e & ~(long long)(LW::EPV - 1);
     lw.sh = (int)(e - ea);
     // exact span of elements the taps read (relative to the block base)
     // (selects on floats first: a NaN/huge float must never reach an integer cast)
     const float f0 = lw.inwin ? floorf(lw.xp[0]) : 0.0f;
     const float f1 = lw.inwin ? floorf(lw.xp[LW::T - 1]) : 0.0f;
-    const long long first = lrow * W + (long long)f0;
-    const long long last = lrow * W + (long long)f1 + 1;
-    const char *base = reinterpret_cast<const char *>(a.lvl[i]) + pblk * W * LW::ES;
-    const auto rs = make_rsrc(base, clamp_bytes((a.P - pblk) * (long long)W * LW::ES));
+    const long long first = lrow * ld + (long long)f0;
+    const long long last = lrow * ld + (long long)f1 + 1;
+    const char *base = reinterpret_cast<const char *>(a.lvl[i]) + pblk * ld * LW::ES;
+    const auto rs = make_rsrc(base, clamp_bytes((a.P - pblk) * ld * LW::ES));
 #pragma unroll
     for (int k = 0; k < LW::NV; ++k) {
         const long long c0 = ea + (long long)k * LW::EPV;
@@ -127,8 +128,8 @@ __device__ __forceinline__ void finish_level(const LevelWindow<R, BF16> &lw, con
         const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
         if (__builtin_expect(lw.inwin && (x0 < nt - 1.0f || x0 > nt + 1.0f), 0)) {
             // Guarded scalar fallback (never taken within the error bound).
-            const char *base = reinterpret_cast<const char *>(a.lvl[i]) + pblk * W * LW::ES;
-            const long long k0 = lrow * W + (long long)x0;
+            const char *base = reinterpret_cast<const char *>(a.lvl[i]) + pblk * a.ld[i] * LW::ES;
+            const long long k0 = lrow * a.ld[i] + (long long)x0;
             if constexpr (BF16) {
                 const uint16_t *rowp = reinterpret_cast<const uint16_t *>(base);
                 a0 = ok0 ? bf16_to_f32(rowp[k0]) : 0.0f;

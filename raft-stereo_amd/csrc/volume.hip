@@ -34,22 +34,65 @@
 namespace rc {
 
 // Dev-only ablation flags (RAFTCORR_BUILD_MODE): 1 = no operand loads,
-// 2 = no epilogue stores, 8 = old register epilogue (narrow per-lane stores
-// for levels >= 1).  Product launches use 0.
-enum { kModeNoLoads = 1, kModeNoStores = 2, kModeRegEpilogue = 8, kModeNtStores = 32 };
+// 2 = no epilogue stores.  Product launches use 0.
+enum { kModeNoLoads = 1, kModeNoStores = 2, kModeStagger = 64 };
+
+// First-round stagger: workgroup slot k of a CU (blockIdx / nCU) waits k
+// units before starting, so the co-resident workgroups of a CU sit in
+// different phases (load / MFMA / store) instead of in lockstep; later
+// workgroups inherit the offset when they take a finished slot.
+__device__ __forceinline__ void stagger_start(int bid, int ncu, int unit_sleeps) {
+    const int slot = bid / ncu;
+    if (slot >= 1 && slot <= 2) {
+        const int n = slot * unit_sleeps;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);  // ~8k cycles each
+    }
+}
 
 constexpr int kStageFloats = 64 * 32;  // per-wave LDS staging: one 64x32 fp32 level-1 tile
 
-// Store level l of a wave tile from its LDS staging image [FM*16 rows][64>>l]
-// as whole-row vector stores: VW floats per lane (VW | W2>>l, so every vector
-// is aligned and either fully inside or fully outside the row), 64/(cw/VW)
-// rows per wave instruction.
-template <int FM, int VW, bool NT>
-__device__ __forceinline__ void store_staged(const float *st, int l, void *lvl, int bf16,
-                                             long long rowbase, int m0, int n0, int W1, int W2,
-                                             int lane) {
-    const int cw = 64 >> l, Wl = W2 >> l;
-    constexpr int lvw = VW == 4 ? 2 : (VW == 2 ? 1 : 0);
+// VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
+template <int VW>
+__device__ __forceinline__ void store_vec(void *lvl, bool bf16, long long g, const float *v) {
+    if (bf16) {
+        uint16_t *d = reinterpret_cast<uint16_t *>(lvl) + g;
+        if constexpr (VW == 1) {
+            d[0] = f32_to_bf16(v[0]);
+        } else {
+            unsigned w[VW / 2];
+#pragma unroll
+            for (int k = 0; k < VW / 2; ++k)
+                w[k] = (unsigned)f32_to_bf16(v[2 * k]) | ((unsigned)f32_to_bf16(v[2 * k + 1]) << 16);
+            if constexpr (VW == 8) *reinterpret_cast<uint4 *>(d) = uint4{w[0], w[1], w[2], w[3]};
+            else if constexpr (VW == 4) *reinterpret_cast<uint2 *>(d) = uint2{w[0], w[1]};
+            else *reinterpret_cast<unsigned *>(d) = w[0];
+        }
+    } else {
+        float *d = reinterpret_cast<float *>(lvl) + g;
+        if constexpr (VW >= 4) {
+#pragma unroll
+            for (int k = 0; k < VW; k += 4)
+                *reinterpret_cast<f32x4 *>(d + k) = f32x4{v[k], v[k + 1], v[k + 2], v[k + 3]};
+        } else if constexpr (VW == 2) {
+            *reinterpret_cast<f32x2 *>(d) = f32x2{v[0], v[1]};
+        } else {
+            d[0] = v[0];
+        }
+    }
+}
+
+// Store level l of a wave tile from its LDS staging image [FM*16 rows][cw =
+// 64>>l] as whole-row vector stores of VW elements per lane, 64/(cw/VW) rows
+// per wave instruction.  VW divides the row stride ld and the tile column
+// offset, so every vector is aligned; a vector that starts inside the row
+// (col < Wl) is written whole -- its tail lands in the row's padding
+// (ld >= round_up(Wl, VW) by construction).
+template <int FM, int VW>
+__device__ __forceinline__ void store_staged(const float *st, int l, void *lvl, long long ld,
+                                             bool bf16, long long rowbase, int m0, int n0, int W1,
+                                             int Wl, int lane) {
+    const int cw = 64 >> l;
+    constexpr int lvw = VW == 8 ? 3 : (VW == 4 ? 2 : (VW == 2 ? 1 : 0));
     const int llpr = 6 - l - lvw;     // log2(lanes per row)
     const int rpi = 64 >> llpr;       // rows per instruction
     const int Rl = lane >> llpr, j = (lane & ((1 << llpr) - 1)) * VW;
@@ -58,38 +101,27 @@ __device__ __forceinline__ void store_staged(const float *st, int l, void *lvl, 
         const int R = r0 + Rl;
         const int w1 = m0 + R;
         if (R < FM * 16 && w1 < W1 && col < Wl) {
-            const long long g = (rowbase + w1) * Wl + col;
-            const float *src = st + R * cw + j;
-            if (bf16) {
+            float v[VW];
 #pragma unroll
-                for (int c = 0; c < VW; ++c)
-                    reinterpret_cast<uint16_t *>(lvl)[g + c] = f32_to_bf16(src[c]);
-            } else if constexpr (VW == 4) {
-                f32x4 *d = reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(lvl) + g);
-                const f32x4 v = *reinterpret_cast<const f32x4 *>(src);
-                if constexpr (NT) __builtin_nontemporal_store(v, d);
-                else *d = v;
-            } else if constexpr (VW == 2) {
-                *reinterpret_cast<f32x2 *>(reinterpret_cast<float *>(lvl) + g) =
-                    *reinterpret_cast<const f32x2 *>(src);
-            } else {
-                reinterpret_cast<float *>(lvl)[g] = src[0];
-            }
+            for (int c = 0; c < VW; ++c) v[c] = st[R * cw + j + c];
+            store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v);
         }
     }
 }
 
-template <int FM, bool NT>
-__device__ __forceinline__ void store_staged_any(const float *st, int l, void *lvl, int bf16,
-                                                 long long rowbase, int m0, int n0, int W1,
-                                                 int W2, int lane) {
-    const int Wl = W2 >> l, cw = 64 >> l;
-    if (Wl % 4 == 0 && cw >= 4)
-        store_staged<FM, 4, NT>(st, l, lvl, bf16, rowbase, m0, n0, W1, W2, lane);
-    else if (Wl % 2 == 0 && cw >= 2)
-        store_staged<FM, 2, NT>(st, l, lvl, bf16, rowbase, m0, n0, W1, W2, lane);
+template <int FM>
+__device__ __forceinline__ void store_staged_any(const float *st, int l, void *lvl, long long ld,
+                                                 bool bf16, long long rowbase, int m0, int n0,
+                                                 int W1, int Wl, int lane) {
+    const int cw = 64 >> l;
+    if (bf16 && ld % 8 == 0 && cw >= 8)
+        store_staged<FM, 8>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
+    else if (ld % 4 == 0 && cw >= 4)
+        store_staged<FM, 4>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
+    else if (ld % 2 == 0 && cw >= 2)
+        store_staged<FM, 2>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
     else
-        store_staged<FM, 1, NT>(st, l, lvl, bf16, rowbase, m0, n0, W1, W2, lane);
+        store_staged<FM, 1>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
 }
 
 template <int N>
@@ -122,13 +154,6 @@ __device__ __forceinline__ typename FragVec<N>::T load_frag(__amdgpu_buffer_rsrc
         for (int c = 0; c < N; ++c) v[c] = ld1(r, off + 4 * c);
     }
     return v;
-}
-
-__device__ __forceinline__ void store_level(void *lvl, int bf16, long long idx, float v) {
-    if (bf16)
-        reinterpret_cast<uint16_t *>(lvl)[idx] = f32_to_bf16(v);
-    else
-        reinterpret_cast<float *>(lvl)[idx] = v;
 }
 
 template <int FM, int U>
@@ -171,23 +196,23 @@ __device__ __forceinline__ void mma_stage(const Stage<FM, U> &s, f32x4 (&acc)[FM
 // acc[ma][nb] register r of lane l holds C[m0 + R][n0 + 4*(l&15) + nb] with
 // R = FM*((l>>4)*4 + r) + ma (interleaved rows, fp32 kernel) or
 // R = 16*ma + (l>>4)*4 + r (blocked rows, bf16 kernel).
-template <int FM, int MODE, bool BLOCKED, bool VEC>
+template <int FM, int MODE, bool BLOCKED>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildArgs &a, int row,
                                          int m0, int n0, int lane, float *stA, float *stB) {
     const int W1 = a.W1, W2 = a.W2;
-    const int wb = n0 + 4 * (lane & 15);  // this lane's w2 quad
+    const int wb = n0 + 4 * (lane & 15);            // this lane's w2 quad
     const long long rowbase = (long long)row * W1;  // pyramid row of w1 = 0
     const int col = lane & 15;
     const bool bf = a.pyr_bf16 != 0;
-    constexpr bool kStaged = !(MODE & kModeRegEpilogue);
+    const long long ld0 = a.ld[0];
+    const bool vec0 = (ld0 & 3) == 0;               // quad stores stay aligned
 #pragma unroll
     for (int ma = 0; ma < FM; ++ma) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int R = BLOCKED ? 16 * ma + (lane >> 4) * 4 + r
-                              : FM * ((lane >> 4) * 4 + r) + ma;  // tile row (w1 - m0)
+                                  : FM * ((lane >> 4) * 4 + r) + ma;  // tile row (w1 - m0)
             const int w1 = m0 + R;
-            const bool rv = w1 < W1;
             const long long p = rowbase + w1;
             float c[4];
 #pragma unroll
@@ -200,56 +225,28 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
                 asm volatile("" ::"v"(keep));
                 continue;
             }
-            // level 0: 4 consecutive w2 per lane, 16 lanes = 256 contiguous bytes
-            if (rv) {
-                if (!bf && VEC && wb + 3 < W2) {
-                    f32x4 *d = reinterpret_cast<f32x4 *>(reinterpret_cast<float *>(a.lvl[0]) + p * W2 + wb);
-                    if constexpr ((MODE & kModeNtStores) != 0) __builtin_nontemporal_store(f32x4{c[0], c[1], c[2], c[3]}, d);
-                    else *d = f32x4{c[0], c[1], c[2], c[3]};
+            // level 0: 4 consecutive w2 per lane, 16 lanes = one 64-wide row segment
+            if (w1 < W1 && wb < W2) {
+                if (vec0) {
+                    store_vec<4>(a.lvl[0], bf, p * ld0 + wb, c);
                 } else {
 #pragma unroll
                     for (int nb = 0; nb < 4; ++nb)
-                        if (wb + nb < W2) store_level(a.lvl[0], bf, p * W2 + wb + nb, c[nb]);
+                        if (wb + nb < W2) store_vec<1>(a.lvl[0], bf, p * ld0 + wb + nb, &c[nb]);
                 }
             }
             if (a.nfused < 2) continue;
-            // level 1: lane-local pairs
-            const float e0 = (c[0] + c[1]) * 0.5f, e1 = (c[2] + c[3]) * 0.5f;
-            if constexpr (kStaged) {
-                // stage into this wave's LDS image [R][32]; stored as whole rows below
-                *reinterpret_cast<f32x2 *>(stA + R * 32 + 2 * col) = f32x2{e0, e1};
-                continue;
-            } else {
-                const int Wl = W2 >> 1, j = wb >> 1;
-                if (rv) {
-                    if (j < Wl) store_level(a.lvl[1], bf, p * Wl + j, e0);
-                    if (j + 1 < Wl) store_level(a.lvl[1], bf, p * Wl + j + 1, e1);
-                }
-                if (a.nfused < 3) continue;
-                float f = (e0 + e1) * 0.5f;
-                {
-                    const int Wl2 = W2 >> 2, j2 = wb >> 2;
-                    if (rv && j2 < Wl2) store_level(a.lvl[2], bf, p * Wl2 + j2, f);
-                }
-#pragma unroll
-                for (int l = 3; l < 7; ++l) {
-                    if (a.nfused <= l) break;                 // wave-uniform
-                    const int m = 1 << (l - 3);               // lane distance
-                    const float o = __shfl_xor(f, m);
-                    f = (f + o) * 0.5f;
-                    const int Wl3 = W2 >> l, j3 = wb >> l;
-                    if (rv && (col & (2 * m - 1)) == 0 && j3 < Wl3)
-                        store_level(a.lvl[l], bf, p * Wl3 + j3, f);
-                }
-            }
+            // level 1 (lane-local pairs), staged in this wave's LDS image [R][32]
+            *reinterpret_cast<f32x2 *>(stA + R * 32 + 2 * col) =
+                f32x2{(c[0] + c[1]) * 0.5f, (c[2] + c[3]) * 0.5f};
         }
     }
-    if constexpr (kStaged && !(MODE & kModeNoStores)) {
+    if constexpr (!(MODE & kModeNoStores)) {
         if (a.nfused < 2) return;
         // Levels >= 1 from the wave-private LDS images (in-order LDS within a
         // wave: no barrier needed).  Level l+1 = pairwise mean of level l,
-        // read back from LDS: the same fp32 ops as the register path.
-        store_staged_any<FM, (MODE & kModeNtStores) != 0>(stA, 1, a.lvl[1], bf, rowbase, m0, n0, W1, W2, lane);
+        // read back from LDS in fp32: the same ops as avg_pool2d (:294).
+        store_staged_any<FM>(stA, 1, a.lvl[1], a.ld[1], bf, rowbase, m0, n0, W1, W2 >> 1, lane);
         float *src = stA, *dst = stB;
         for (int l = 2; l < a.nfused; ++l) {
             const int cw = 64 >> l, cwp = 2 * cw;
@@ -259,14 +256,13 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
                 const f32x2 pr = *reinterpret_cast<const f32x2 *>(src + R * cwp + 2 * j);
                 dst[R * cw + j] = (pr[0] + pr[1]) * 0.5f;
             }
-            store_staged_any<FM, (MODE & kModeNtStores) != 0>(dst, l, a.lvl[l], bf, rowbase, m0, n0, W1, W2, lane);
+            store_staged_any<FM>(dst, l, a.lvl[l], a.ld[l], bf, rowbase, m0, n0, W1, W2 >> l, lane);
             float *t = src;
             src = dst;
             dst = t;
         }
     }
 }
-
 
 template <int FM, int U, bool VEC, int MODE>
 __device__ __forceinline__ void wave_tile(const BuildArgs &a, int row, int b, int h, int m0,
@@ -299,11 +295,12 @@ __device__ __forceinline__ void wave_tile(const BuildArgs &a, int row, int b, in
         }
     }
 
-    epilogue<FM, MODE, false, VEC>(acc, a, row, m0, n0, lane, stA, stB);
+    epilogue<FM, MODE, false>(acc, a, row, m0, n0, lane, stA, stB);
 }
 
 template <bool VEC, int U, int MODE>
 __global__ __launch_bounds__(256) void build_f32_kernel(BuildArgs a, int nwg_total) {
+    if constexpr ((MODE & kModeStagger) != 0) stagger_start(blockIdx.x, 256, a.stagger);
     // one LDS array (guide §5 trap 4a): per wave an 8 KB + 4 KB ping-pong
     // staging image for the pooled levels
     __shared__ __attribute__((aligned(16))) float smem[4][kStageFloats + kStageFloats / 2];
@@ -451,6 +448,11 @@ __device__ __forceinline__ void wave_tile_bf16(const BuildArgs &a, int row, int 
     // staging assignment: chunk c = lane + 64t (t = 0..3) -> d-row c>>3, w chunk c&7
     u32x4 ra[4], rb[4];
     auto load_step = [&](int k0) {
+        if constexpr ((MODE & kModeNoLoads) != 0) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) { ra[t] = u32x4{(unsigned)k0, 1u, 2u, (unsigned)lane}; rb[t] = ra[t]; }
+            return;
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int c = lane + 64 * t, d = k0 + (c >> 3), m = c & 7;
@@ -496,7 +498,7 @@ __device__ __forceinline__ void wave_tile_bf16(const BuildArgs &a, int row, int 
             for (int nb = 0; nb < 4; ++nb)
                 acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ma], fb[nb], acc[ma][nb], 0, 0, 0);
     }
-    epilogue<4, MODE, true, ALIGNED>(acc, a, row, m0, n0, lane, stA, stB);
+    epilogue<4, MODE, true>(acc, a, row, m0, n0, lane, stA, stB);
 }
 
 template <bool IN_BF16, bool ALIGNED, int MODE>
@@ -520,14 +522,161 @@ __global__ __launch_bounds__(256) void build_bf16_kernel(BuildArgs a, int nwg_to
     wave_tile_bf16<IN_BF16, ALIGNED, MODE>(a, row, b, h, m0, n0, lane, img, stA, stB);
 }
 
+// ============ fp32 MFMA with a workgroup LDS-DMA ring (default) ============
+//
+// Operand tiles are shared by the workgroup's four waves through a 3-slot LDS
+// ring filled by buffer->LDS DMA (buffer_load_dwordx4 ... lds): slot = a
+// [16 d][128 w] tile of F1 and of F2 (16 KB), two stages in flight ahead of
+// the one being multiplied, no VGPR staging.  Stage s+2 is issued into the
+// slot stage s-1 used, after the barrier that follows every wave's counted
+// vmcnt for stage s (RAW) and its lgkmcnt(0) for the reads of stage s-1
+// (WAR) -- cdna_hip_programming.md §5 "Pipelining across barriers".
+// Fragments are read with ds_read_b128 (conflict-free: the 16-lane groups of
+// a b128 read cover all 64 banks of two 512-B rows).  Waves with no valid
+// rows still issue their share of the DMA and join every barrier.
+constexpr int kRingSlots = 3;
+constexpr int kBK = 16;                       // d rows per ring stage
+constexpr int kSlotFloats = 2 * kBK * 128;    // A + B tiles of one stage
+static_assert(kRingSlots * kSlotFloats >= 4 * (kStageFloats + kStageFloats / 2),
+              "epilogue staging must fit in the ring");
+
+template <int FM>
+__device__ __forceinline__ void ring_stage(const float *sA, const float *sB, int am, int bn,
+                                           int lane, f32x4 (&acc)[FM][4]) {
+#pragma unroll
+    for (int kk = 0; kk < kBK / 4; ++kk) {
+        const int dr = 4 * kk + (lane >> 4);
+        const float *pa = sA + dr * 128 + am + FM * (lane & 15);
+        float av[4];
+        if constexpr (FM == 4) {
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(pa);
+            av[0] = v[0]; av[1] = v[1]; av[2] = v[2]; av[3] = v[3];
+        } else if constexpr (FM == 2) {
+            const f32x2 v = *reinterpret_cast<const f32x2 *>(pa);
+            av[0] = v[0]; av[1] = v[1];
+        } else {
+#pragma unroll
+            for (int c = 0; c < FM; ++c) av[c] = pa[c];
+        }
+        const f32x4 bv = *reinterpret_cast<const f32x4 *>(sB + dr * 128 + bn + 4 * (lane & 15));
+#pragma unroll
+        for (int ma = 0; ma < FM; ++ma)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+                acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ma], bv[nb], acc[ma][nb], 0, 0, 0);
+    }
+}
+
+struct RingCtx {
+    __amdgpu_buffer_rsrc_t r1, r2;
+    int D, H, h, W1, W2, M0, N0, wave, lane, nst;
+};
+
+// DMA share of this wave per stage: rows 4w..4w+3 of both tiles, 2 rows
+// (1 KB = 64 lanes x 16 B) per instruction -> 4 instructions per stage.
+__device__ __forceinline__ void ring_issue(const RingCtx &c, float *smem, int st) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    float *sA = smem + (st % kRingSlots) * kSlotFloats, *sB = sA + kBK * 128;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r0 = 4 * c.wave + 2 * i;
+        const int d = st * kBK + r0 + (c.lane >> 5);
+        const int w = 4 * (c.lane & 31);
+        const long long base = (long long)(d < c.D ? d : 0) * c.H + c.h;
+        const uint32_t offA = d < c.D ? (uint32_t)((base * c.W1 + c.M0 + w) * 4) : 0xFFFFFF00u;
+        const uint32_t offB = d < c.D ? (uint32_t)((base * c.W2 + c.N0 + w) * 4) : 0xFFFFFF00u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r1, (lds_void *)(sA + r0 * 128), 16, (int)offA, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r2, (lds_void *)(sB + r0 * 128), 16, (int)offB, 0, 0, 0);
+    }
+}
+
+// The whole K loop + epilogue for one wave with FM A-fragments (FM = 0: a
+// wave with no valid rows -- it still issues its DMA share and joins every
+// barrier, so all four waves execute the same barrier sequence).
+template <int FM, int MODE>
+__device__ __forceinline__ void ring_body(const RingCtx &c, const BuildArgs &a, float *smem, int row,
+                                          int am, int bn) {
+    f32x4 acc[FM > 0 ? FM : 1][4];
+#pragma unroll
+    for (int i = 0; i < (FM > 0 ? FM : 1); ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ring_issue(c, smem, 0);
+    if (c.nst > 1) ring_issue(c, smem, 1);
+    for (int st = 0; st < c.nst; ++st) {
+        // RAW: my DMA for stage st landed (stage st+1's 4 may stay in flight);
+        // WAR: my LDS reads of stage st-1 are done.  Then the barrier.
+        if (st + 1 < c.nst) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (st + 2 < c.nst) ring_issue(c, smem, st + 2);
+        if constexpr (FM > 0) {
+            const float *sA = smem + (st % kRingSlots) * kSlotFloats, *sB = sA + kBK * 128;
+            ring_stage<FM>(sA, sB, am, bn, c.lane, acc);
+        }
+    }
+    // everyone is done with the ring before it becomes epilogue staging
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if constexpr (FM > 0) {
+        float *stA = smem + c.wave * (kStageFloats + kStageFloats / 2), *stB = stA + kStageFloats;
+        epilogue<FM, MODE, false>(acc, a, row, c.M0 + am, c.N0 + bn, c.lane, stA, stB);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void build_f32_ring_kernel(BuildArgs a, int nwg_total) {
+    __shared__ __attribute__((aligned(16))) float smem[kRingSlots * kSlotFloats];
+    RingCtx c;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.lane = threadIdx.x & 63;
+    const int T = a.tiles_m * a.tiles_n;
+    const int v = blockIdx.x;
+    const int xcd = v & 7, q = nwg_total >> 3, rr = nwg_total & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (v >> 3);
+    const int row = wgid / T, tile = wgid - row * T;
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int b = row / a.H;
+    c.h = row - b * a.H;
+    c.D = a.D; c.H = a.H; c.W1 = a.W1; c.W2 = a.W2;
+    c.M0 = tm * 128; c.N0 = tn * 128;
+    c.nst = (a.D + kBK - 1) / kBK;
+    const long long img1 = (long long)a.D * a.H * a.W1, img2 = (long long)a.D * a.H * a.W2;
+    c.r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
+    c.r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
+    const int am = (c.wave >> 1) * 64, bn = (c.wave & 1) * 64;   // wave tile in the WG tile
+    const int m0 = c.M0 + am, n0 = c.N0 + bn;
+    const int rows = a.W1 - m0;
+    const bool active = rows > 0 && n0 < a.W2;                    // wave-uniform
+    if (!active) ring_body<0, MODE>(c, a, smem, row, am, bn);
+    else if (rows > 48) ring_body<4, MODE>(c, a, smem, row, am, bn);
+    else if (rows > 32) ring_body<3, MODE>(c, a, smem, row, am, bn);
+    else if (rows > 16) ring_body<2, MODE>(c, a, smem, row, am, bn);
+    else ring_body<1, MODE>(c, a, smem, row, am, bn);
+}
+
 template <bool VEC, int U, int MODE>
 static void launch(const BuildArgs &a, unsigned nwg, hipStream_t s) {
     hipLaunchKernelGGL((build_f32_kernel<VEC, U, MODE>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
 }
 
+template <int MODE>
+static void launch_ring(const BuildArgs &a, unsigned nwg, hipStream_t s) {
+    hipLaunchKernelGGL((build_f32_ring_kernel<MODE>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
+}
+
 template <bool IN_BF16, bool ALIGNED>
 static void launch_bf16(const BuildArgs &a, unsigned nwg, hipStream_t s) {
-    hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 0>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
+    int mode = 0;
+    if (const char *e = getenv("RAFTCORR_BUILD_MODE")) mode = atoi(e);
+    switch (mode) {   // dev-only ablation (see rc_launch_build_f32)
+        case 1: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 1>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
+        case 2: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 2>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
+        case 3: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 3>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
+        default: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 0>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
+    }
 }
 
 }  // namespace rc
@@ -547,9 +696,9 @@ hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStrea
     return hipGetLastError();
 }
 
-// RAFTCORR_BUILD_MODE (dev-only ablation, read per call): flags 1 no operand
-// loads, 2 no epilogue stores, 4 prefetch U=4 (default U=2), 8 register
-// epilogue, 32 non-temporal pyramid stores.  0 = product.
+// RAFTCORR_BUILD_MODE (dev-only ablation, read per call): 0 = product (LDS-DMA
+// ring kernel), 2 = ring without epilogue stores; 128+flags = the direct-load
+// kernel (flags 1 no operand loads, 2 no stores, 64 stagger).
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
     const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
     if (nwg <= 0) return hipSuccess;
@@ -562,14 +711,13 @@ hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
         rc::launch<false, 2, 0>(a, n, s);
     } else {
         switch (mode) {
-            case 1: rc::launch<true, 2, 1>(a, n, s); break;
-            case 2: rc::launch<true, 2, 2>(a, n, s); break;
-            case 3: rc::launch<true, 2, 3>(a, n, s); break;
-            case 4: rc::launch<true, 4, 0>(a, n, s); break;
-            case 8: rc::launch<true, 2, 8>(a, n, s); break;
-            case 12: rc::launch<true, 4, 8>(a, n, s); break;
-            case 32: rc::launch<true, 2, 32>(a, n, s); break;
-            default: rc::launch<true, 2, 0>(a, n, s); break;
+            case 2: rc::launch_ring<2>(a, n, s); break;
+            case 128: rc::launch<true, 2, 0>(a, n, s); break;      // direct-load kernel
+            case 130: rc::launch<true, 2, 2>(a, n, s); break;
+            case 131: rc::launch<true, 2, 3>(a, n, s); break;
+            case 129: rc::launch<true, 2, 1>(a, n, s); break;
+            case 192: rc::launch<true, 2, 64>(a, n, s); break;
+            default: rc::launch_ring<0>(a, n, s); break;
         }
     }
     return hipGetLastError();

@@ -40,7 +40,7 @@ def _build(**kw):
     args.update(kw)
     ptrs = _lib.ptr_array([None] * max(args["nbuf"], 1)) if args["pyr"] is None else args["pyr"]
     return _lib.lib().rc_corr_build(args["f1"], args["f2"], args["dt"], args["B"], args["D"],
-                                    args["H"], args["W1"], args["W2"], ptrs, args["nbuf"],
+                                    args["H"], args["W1"], args["W2"], ptrs, None, args["nbuf"],
                                     args["pdt"], None)
 
 
@@ -66,18 +66,23 @@ def test_lookup_validation():
     L = _lib.lib()
     ptrs = _lib.ptr_array([None])
     w = _lib.int_array([8])
-    assert L.rc_corr_lookup(ptrs, w, 0, 0, 4, None, 0, 1, 1, 8, None, None) == _lib.RC_EINVAL
-    assert L.rc_corr_lookup(ptrs, w, 0, 1, 9, None, 0, 1, 1, 8, None, None) == _lib.RC_EUNSUPPORTED
-    assert L.rc_corr_lookup(ptrs, w, 3, 1, 4, None, 0, 1, 1, 8, None, None) == _lib.RC_EINVAL
-    assert L.rc_corr_lookup(ptrs, w, 0, 1, 4, None, 0, 0, 1, 8, None, None) == _lib.RC_OK
+    assert L.rc_corr_lookup(ptrs, w, None, 0, 0, 4, None, 0, 1, 1, 8, None, None) == _lib.RC_EINVAL
+    assert L.rc_corr_lookup(ptrs, w, None, 0, 1, 9, None, 0, 1, 1, 8, None, None) == _lib.RC_EUNSUPPORTED
+    assert L.rc_corr_lookup(ptrs, w, None, 3, 1, 4, None, 0, 1, 1, 8, None, None) == _lib.RC_EINVAL
+    assert L.rc_corr_lookup(ptrs, w, None, 0, 1, 4, None, 0, 0, 1, 8, None, None) == _lib.RC_OK
     # misaligned level pointer is rejected before any launch
     bad = _lib.ptr_array([ctypes.c_void_p(0x1004)])
-    assert L.rc_corr_lookup(bad, w, 0, 1, 4, ctypes.c_void_p(0x2000), 0, 1, 1, 8,
+    assert L.rc_corr_lookup(bad, w, None, 0, 1, 4, ctypes.c_void_p(0x2000), 0, 1, 1, 8,
                             ctypes.c_void_p(0x3000), None) == _lib.RC_EINVAL
     assert b"aligned" in L.rc_last_error()
+    # a row stride below the width is rejected
+    good = _lib.ptr_array([ctypes.c_void_p(0x1000)])
+    assert L.rc_corr_lookup(good, w, _lib.long_array([7]), 0, 1, 4, ctypes.c_void_p(0x2000), 0, 1,
+                            1, 8, ctypes.c_void_p(0x3000), None) == _lib.RC_EINVAL
 
 
 def test_pool_validation():
     L = _lib.lib()
-    assert L.rc_corr_pool(None, None, 4, 1, 0, None) == _lib.RC_EINVAL
-    assert L.rc_corr_pool(None, None, 0, 8, 0, None) == _lib.RC_OK
+    assert L.rc_corr_pool(None, 1, None, 1, 4, 1, 0, None) == _lib.RC_EINVAL
+    assert L.rc_corr_pool(None, 8, None, 4, 0, 8, 0, None) == _lib.RC_OK
+    assert L.rc_corr_pool(None, 7, None, 4, 0, 8, 0, None) == _lib.RC_EINVAL   # ld_in < W_in

@@ -37,13 +37,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--build-modes", default="0,32,8,4,2,1,3")
     ap.add_argument("--lookup-variants", default="0,1,3")
+    ap.add_argument("--staggers", default="", help="RAFTCORR_STAGGER values to try with mode 64")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
     B, D, H, W1, W2, L, r, iters, _ = cfg
     dev = torch.device("cuda", 0)
     res = {}
+    bf16 = a.config in bench.BF16_CONFIGS
     with torch.no_grad():
-        f1, f2, coords = bench.make_inputs(cfg, dev, seed=1)
+        f1, f2, coords = bench.make_inputs(cfg, dev, seed=1,
+                                           dtype=torch.bfloat16 if bf16 else torch.float32)
         ref_blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
         ref_out = ref_blk(coords[0])
         bm = [int(x) for x in a.build_modes.split(",") if x]
@@ -51,7 +54,7 @@ def main():
         for m in bm:  # warm + correctness of product-equivalent modes
             os.environ["RAFTCORR_BUILD_MODE"] = str(m)
             blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
-            if m in (0, 4, 8, 32):
+            if m in (0, 128):
                 for i in range(L + 1):
                     assert torch.equal(blk.corr_pyramid[i], ref_blk.corr_pyramid[i]), (m, i)
         os.environ["RAFTCORR_BUILD_MODE"] = "0"
@@ -59,11 +62,18 @@ def main():
             os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
             out = ref_blk(coords[0])
             assert torch.equal(out, ref_out), v
+        stg = [int(x) for x in a.staggers.split(",") if x]
         for rnd in range(a.rounds):
             for m in bm:
                 os.environ["RAFTCORR_BUILD_MODE"] = str(m)
                 t = time_launches(lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r), 3)
                 res.setdefault(f"build_mode{m}", []).extend(t)
+            for sv in stg:
+                os.environ["RAFTCORR_BUILD_MODE"] = "64"
+                os.environ["RAFTCORR_STAGGER"] = str(sv)
+                t = time_launches(lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r), 3)
+                res.setdefault(f"build_stagger{sv}", []).extend(t)
+            os.environ.pop("RAFTCORR_STAGGER", None)
             os.environ["RAFTCORR_BUILD_MODE"] = "0"
             for v in lv:
                 os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
