@@ -148,10 +148,11 @@ __device__ __forceinline__ void finish_level(const LevelWindow<R, BF16> &lw, con
 }
 
 // NL > 0: compile-time level count (all loads issue first); NL == 0: runtime.
-template <int R, int NL, bool BF16, bool EXACT>
-__global__ __launch_bounds__(256) void lookup_kernel(LookupArgs a) {
+// BS = threads per block (256 for throughput, 64 to spread small problems).
+template <int R, int NL, bool BF16, bool EXACT, int BS = 256>
+__global__ __launch_bounds__(BS) void lookup_kernel(LookupArgs a) {
     constexpr int T = 2 * R + 1;
-    const long long pblk = (long long)blockIdx.x * 256;
+    const long long pblk = (long long)blockIdx.x * BS;
     const long long p = pblk + threadIdx.x;
     const bool active = p < a.P;
     const long long pp = active ? p : a.P - 1;
@@ -175,18 +176,32 @@ __global__ __launch_bounds__(256) void lookup_kernel(LookupArgs a) {
     }
 }
 
-template <int R, int NL, bool BF16, bool EXACT>
+template <int R, int NL, bool BF16, bool EXACT, int BS = 256>
 static void launch_k(const LookupArgs &a, hipStream_t s) {
-    const unsigned nblk = (unsigned)((a.P + 255) / 256);
-    hipLaunchKernelGGL((lookup_kernel<R, NL, BF16, EXACT>), dim3(nblk), dim3(256), 0, s, a);
+    const unsigned nblk = (unsigned)((a.P + BS - 1) / BS);
+    hipLaunchKernelGGL((lookup_kernel<R, NL, BF16, EXACT, BS>), dim3(nblk), dim3(BS), 0, s, a);
 }
+
+// Below this many pixels the launch cannot fill the chip with the 256-thread
+// runtime-loop kernel (one dependent memory round trip per level): use
+// 64-thread blocks and issue every level's loads up front instead.
+constexpr long long kSmallP = 256LL * 256 * 2;
 
 template <int R>
 static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream_t s) {
     // Default: runtime level loop (low VGPR count, 8 waves/SIMD) + exact-span
     // predicated loads.  Variant 1: full windows; 3: levels unrolled (all
     // loads first; ~130 VGPRs).  Measured (tools/ablate.py) before choosing.
-    if (variant == 1) {
+    const bool unroll = a.levels == 3 || a.levels == 4;
+    if (variant == 0 && a.P < kSmallP && unroll) {
+        if (a.levels == 4) {
+            if (bf16) launch_k<R, 4, true, true, 64>(a, s);
+            else launch_k<R, 4, false, true, 64>(a, s);
+        } else {
+            if (bf16) launch_k<R, 3, true, true, 64>(a, s);
+            else launch_k<R, 3, false, true, 64>(a, s);
+        }
+    } else if (variant == 1) {
         if (bf16) launch_k<R, 0, true, false>(a, s);
         else launch_k<R, 0, false, false>(a, s);
     } else if (variant == 3 && a.levels == 4) {

@@ -204,3 +204,26 @@ def test_bf16_mma_vs_oracle(shape, mode):
             assert same(got[i + 1], coracle.corr_pool(got[i]))
     # the lookup reads the stored (bf16 or fp32) pyramid exactly
     assert same(out, coracle.corr_lookup(got[:L], coords.numpy(), L, r))
+
+
+@pytest.mark.parametrize("pyr_dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_lookup_large_p_vs_oracle(pyr_dt):
+    """P above the small-problem threshold takes the 256-thread runtime-level
+    kernel; check it (random pyramid, padded rows, random coords incl. OOB)."""
+    B, H, W1, W2, L, r = 3, 135, 240, 240, 4, 4            # P = 97200 * ... see below
+    B = 6                                                  # P = 194400 > 131072
+    g = torch.Generator().manual_seed(11)
+    P = B * H * W1
+    pyr = []
+    for l in range(L):
+        Wl = W2 >> l
+        buf = torch.randn(P, Wl + 3, generator=g).to(pyr_dt)   # padded rows (stride Wl+3)
+        pyr.append(buf.to(DEV)[:, :Wl].unsqueeze(1).unsqueeze(1))
+    x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 64
+    x[..., ::11] = torch.randint(-20, W2 + 20, x[..., ::11].shape, generator=g).float()
+    coords = torch.cat([x, torch.zeros_like(x)], 1)
+    with torch.no_grad():
+        out = rcorr.lookup(pyr, coords.to(DEV), L, r).cpu().numpy()
+    ref = coracle.corr_lookup([t.reshape(P, -1).float().cpu().numpy() for t in pyr],
+                              coords.numpy(), L, r)
+    assert same(out, ref)
