@@ -10,8 +10,8 @@ Row sharding (config 4): the correlation volume, pyramid and lookup are
 strictly row-local -- row h of fmap1 only meets row h of fmap2
 (model.py:324) and the lookup ignores y (model.py:299, :308) -- so
 ``RowShardedCorr`` builds and looks up only its own block of feature rows,
-again with no exchange.  (The GRU's halo exchange for a fully row-sharded
-network is outside the corr path; see DESIGN.md.)
+again with no exchange.  ``RowShardedStereo`` runs the whole network that
+way, exchanging only the GRU state halos each iteration.
 """
 import torch
 import torch.distributed as dist
@@ -68,3 +68,181 @@ class RowShardedCorr:
 
     def __call__(self, coords):
         return self.block(coords[:, :, self.r0:self.r1].contiguous())
+
+
+# ---------------------------------------------------------------------------
+# Row-sharded network forward (BASELINE config 4: full-resolution, bs=1)
+# ---------------------------------------------------------------------------
+
+def _interp_rows(x, src_lo, src_glob, dst_lo, dst_hi, dst_glob, dst_w):
+    """bilinear, align_corners=True resize of a row SLAB (model.py:184-186)
+    with the GLOBAL row mapping: destination rows [dst_lo, dst_hi) of a level
+    of height dst_glob, from source rows [src_lo, src_lo + x.shape[2]) of a
+    level of height src_glob.  Source rows outside the slab are clamped (only
+    halo rows can need them; the halo absorbs the error)."""
+    scale = (src_glob - 1) / (dst_glob - 1) if dst_glob > 1 else 0.0
+    i = torch.arange(dst_lo, dst_hi, device=x.device, dtype=torch.float32)
+    pos = (i * scale).clamp(max=src_glob - 1)
+    h0 = pos.floor()
+    lam = (pos - h0).view(1, 1, -1, 1)
+    h0 = h0.long()
+    h1 = torch.clamp(h0 + 1, max=src_glob - 1)
+    hs = x.shape[2]
+    l0 = (h0 - src_lo).clamp(0, hs - 1)
+    l1 = (h1 - src_lo).clamp(0, hs - 1)
+    rows = x[:, :, l0] * (1 - lam) + x[:, :, l1] * lam
+    return torch.nn.functional.interpolate(rows, (dst_hi - dst_lo, dst_w), mode="bilinear",
+                                           align_corners=True)
+
+
+class RowShardedStereo:
+    """Row-sharded RAFT-Stereo forward over ``world`` ranks (one per GPU).
+
+    * Encoders (cnet, conv2, context convs) run replicated on the full image,
+      so conv2's InstanceNorm statistics (model.py:35-39, :345) need no
+      exchange (SURVEY.md §8e item 1 sidestepped at the cost of redundant
+      encoder FLOPs).
+    * Rank k owns 1/4-res feature rows [r0, r1) (multiples of 4) and keeps GRU
+      state for the extended slab [r0 - halo, r1 + halo) (1/8 and 1/16 res:
+      halo/2, halo/4).  The correlation pyramid is built for the slab's rows
+      only -- the corr path is row-local (model.py:324, :299/:308).
+    * One iteration on the slab is exact on the owned rows when ``halo``
+      covers the one-iteration dependency cone (<= 20 rows, SURVEY.md §8e);
+      afterwards the owned boundary rows of net[0..2] and coords1 are sent to
+      the two neighbours with point-to-point send/recv (RCCL over xGMI on the
+      GPU box), refreshing their halos.
+    * ``forward`` returns the per-iteration flow of the OWNED rows;
+      ``gather_rows`` assembles full-height tensors.
+    """
+
+    def __init__(self, model, rank, world, halo=32, group=None):
+        if halo % 4:
+            raise ValueError("halo must be a multiple of 4")
+        self.model, self.rank, self.world, self.halo, self.group = model, rank, world, halo, group
+
+    # row geometry -----------------------------------------------------------
+    def _ranges(self, H1):
+        nblk = (H1 + 3) // 4
+        b0, b1 = split_range(nblk, self.rank, self.world)
+        r0, r1 = 4 * b0, min(4 * b1, H1)
+        if self.world > 1 and (r1 - r0) < self.halo and self.rank < self.world - 1:
+            raise ValueError(f"owned rows {r1 - r0} < halo {self.halo}: use fewer ranks or a smaller halo")
+        e0, e1 = max(0, r0 - self.halo), min(H1, r1 + self.halo)
+        return r0, r1, e0, e1
+
+    @staticmethod
+    def _lvl(lo, hi, l):
+        d = 1 << l
+        return lo // d, -(-hi // d)
+
+    def _exchange(self, t, l, own, ext, glob):
+        """Refresh the halo rows of a level-l slab from the two neighbours.
+        Level-l rows: owned [r0, r1), slab [e0, e1), level height ``glob``,
+        halo h = halo >> l.  I send prev my rows [r0, min(glob, r0+h, r1)) (its
+        bottom halo) and next my rows [max(r0, r1-h), r1) (its top halo); I
+        receive [e0, r0) and [r1, e1).  Sizes agree because every rank but
+        the last owns >= halo rows."""
+        if self.world == 1:
+            return t
+        (r0, r1), (e0, e1) = own, ext
+        h = self.halo >> l
+        ops, recv = [], []
+        prev, nxt = self.rank - 1, self.rank + 1
+        if prev >= 0:
+            buf = torch.empty_like(t[:, :, 0:r0 - e0]).contiguous()
+            ops.append(dist.P2POp(dist.irecv, buf, prev, group=self.group))
+            recv.append((buf, 0))
+            hi = min(glob, r0 + h, r1)
+            ops.append(dist.P2POp(dist.isend, t[:, :, r0 - e0:hi - e0].contiguous(), prev,
+                                  group=self.group))
+        if nxt < self.world:
+            buf = torch.empty_like(t[:, :, r1 - e0:e1 - e0]).contiguous()
+            ops.append(dist.P2POp(dist.irecv, buf, nxt, group=self.group))
+            recv.append((buf, r1 - e0))
+            lo = max(r0, r1 - h)
+            ops.append(dist.P2POp(dist.isend, t[:, :, lo - e0:r1 - e0].contiguous(), nxt,
+                                  group=self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        if recv:
+            t = t.clone()
+            for buf, at in recv:
+                t[:, :, at:at + buf.shape[2]] = buf
+        return t
+
+    # forward ----------------------------------------------------------------
+    def forward(self, image1, image2, iters=12):
+        m, a = self.model, self.model.args
+        fmap1, fmap2, net_full, inp_full = m.features(image1, image2)
+        H1 = fmap1.shape[2]
+        r0, r1, e0, e1 = self._ranges(H1)
+        nl = len(net_full)
+        own = [self._lvl(r0, r1, l) for l in range(nl)]
+        ext = [self._lvl(e0, e1, l) for l in range(nl)]
+        glob = [t.shape[2] for t in net_full]
+        net = [net_full[l][:, :, ext[l][0]:ext[l][1]] for l in range(nl)]
+        inp = [[c[:, :, ext[l][0]:ext[l][1]] for c in inp_full[l]] for l in range(nl)]
+        corr_fn = m.corr_block(fmap1[:, :, e0:e1].contiguous(), fmap2[:, :, e0:e1].contiguous(),
+                               radius=a.corr_radius, num_levels=a.corr_levels)
+        B, _, _, W1 = fmap1.shape
+        coords0 = m.initialize_flow(net_full[0])[0][:, :, e0:e1]
+        coords1 = coords0.clone()
+        blk = m.update_block
+        n = a.n_gru_layers
+
+        def interp(x, ls, ld):
+            return _interp_rows(x, ext[ls][0], glob[ls], ext[ld][0], ext[ld][1], glob[ld],
+                                net[ld].shape[3])
+
+        preds = []
+        for _ in range(iters):
+            corr = corr_fn(coords1)
+            flow = coords1 - coords0
+            with m._autocast():
+                if n == 3 and a.slow_fast_gru:
+                    self._gru(blk, net, inp, None, None, interp, True, False, False)
+                if n >= 2 and a.slow_fast_gru:
+                    self._gru(blk, net, inp, None, None, interp, n == 3, True, False)
+                delta = self._gru(blk, net, inp, corr, flow, interp, n == 3, n >= 2, True)
+            delta[:, 1] = 0.0
+            coords1 = coords1 + delta.float()
+            preds.append((coords1 - coords0)[:, :, r0 - e0:r1 - e0])
+            for l in range(nl):
+                net[l] = self._exchange(net[l], l, own[l], ext[l], glob[l])
+            coords1 = self._exchange(coords1, 0, own[0], ext[0], glob[0])
+        return preds
+
+    @staticmethod
+    def _gru(blk, net, inp, corr, flow, interp, iter32, iter16, iter08):
+        """BasicMultiUpdateBlock.forward (model.py:242-265) on a slab, with the
+        global-row interp; returns delta_flow when iter08."""
+        from .network import pool2x
+        n = blk.args.n_gru_layers
+        if iter32:
+            net[2] = blk.gru32(net[2], *inp[2], pool2x(net[1]))
+        if iter16:
+            extra = (interp(net[2], 2, 1),) if n > 2 else ()
+            net[1] = blk.gru16(net[1], *inp[1], pool2x(net[0]), *extra)
+        if iter08:
+            motion = blk.encoder(flow, corr)
+            extra = (interp(net[1], 1, 0),) if n > 1 else ()
+            net[0] = blk.gru08(net[0], *inp[0], motion, *extra)
+            return blk.flow_head(net[0])
+        return None
+
+    def gather_rows(self, local):
+        """all_gather of per-rank owned-row slabs -> full-height tensor."""
+        if self.world == 1:
+            return local
+        n = torch.tensor([local.shape[2]], device=local.device)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(sizes, n, group=self.group)
+        sizes = [int(s.item()) for s in sizes]
+        cap = max(sizes)
+        pad = torch.zeros(local.shape[:2] + (cap,) + local.shape[3:], dtype=local.dtype,
+                          device=local.device)
+        pad[:, :, :local.shape[2]] = local
+        bufs = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(bufs, pad, group=self.group)
+        return torch.cat([b[:, :, :s] for b, s in zip(bufs, sizes)], dim=2)

@@ -68,3 +68,31 @@ def run(rank, world, port, q):
         q.put((rank, repr(e), None))
     finally:
         dist.destroy_process_group()
+
+
+def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4):
+    """Row-sharded network forward vs the unsharded one (oracle corr block)."""
+    import torch
+    import torch.distributed as dist
+    import pkgload
+    pkgload.load()
+    from raft_stereo_amd.shard import RowShardedStereo
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    try:
+        g = torch.Generator().manual_seed(3)
+        img1 = torch.rand(1, 3, H, W, generator=g) * 255
+        img2 = torch.roll(img1, -4, dims=-1)
+        net = model()
+        rs = RowShardedStereo(net, rank, world, halo=halo)
+        with torch.no_grad():
+            preds = rs.forward(img1, img2, iters=iters)
+            full = [rs.gather_rows(p) for p in preds]
+        q.put((rank, torch.stack(full), None))
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
