@@ -540,14 +540,14 @@ constexpr int kSlotFloats = 2 * kBK * 128;    // A + B tiles of one stage
 static_assert(kRingSlots * kSlotFloats >= 4 * (kStageFloats + kStageFloats / 2),
               "epilogue staging must fit in the ring");
 
-template <int FM>
+template <int FM, int FN>
 __device__ __forceinline__ void ring_stage(const float *sA, const float *sB, int am, int bn,
                                            int lane, f32x4 (&acc)[FM][4]) {
 #pragma unroll
     for (int kk = 0; kk < kBK / 4; ++kk) {
         const int dr = 4 * kk + (lane >> 4);
         const float *pa = sA + dr * 128 + am + FM * (lane & 15);
-        float av[4];
+        float av[4], bv[4];
         if constexpr (FM == 4) {
             const f32x4 v = *reinterpret_cast<const f32x4 *>(pa);
             av[0] = v[0]; av[1] = v[1]; av[2] = v[2]; av[3] = v[3];
@@ -558,11 +558,18 @@ __device__ __forceinline__ void ring_stage(const float *sA, const float *sB, int
 #pragma unroll
             for (int c = 0; c < FM; ++c) av[c] = pa[c];
         }
-        const f32x4 bv = *reinterpret_cast<const f32x4 *>(sB + dr * 128 + bn + 4 * (lane & 15));
+        const float *pb = sB + dr * 128 + bn + FN * (lane & 15);
+        if constexpr (FN == 4) {
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(pb);
+            bv[0] = v[0]; bv[1] = v[1]; bv[2] = v[2]; bv[3] = v[3];
+        } else {
+#pragma unroll
+            for (int c = 0; c < FN; ++c) bv[c] = pb[c];
+        }
 #pragma unroll
         for (int ma = 0; ma < FM; ++ma)
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb)
+            for (int nb = 0; nb < FN; ++nb)
                 acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ma], bv[nb], acc[ma][nb], 0, 0, 0);
     }
 }
@@ -590,10 +597,11 @@ __device__ __forceinline__ void ring_issue(const RingCtx &c, float *smem, int st
     }
 }
 
-// The whole K loop + epilogue for one wave with FM A-fragments (FM = 0: a
-// wave with no valid rows -- it still issues its DMA share and joins every
-// barrier, so all four waves execute the same barrier sequence).
-template <int FM, int MODE>
+// The whole K loop + epilogue for one wave with FM A-fragments and FN
+// B-fragments (FM = 0: a wave with no valid rows -- it still issues its DMA
+// share and joins every barrier, so all four waves execute the same barrier
+// sequence).
+template <int FM, int FN, int MODE>
 __device__ __forceinline__ void ring_body(const RingCtx &c, const BuildArgs &a, float *smem, int row,
                                           int am, int bn) {
     f32x4 acc[FM > 0 ? FM : 1][4];
@@ -613,7 +621,7 @@ __device__ __forceinline__ void ring_body(const RingCtx &c, const BuildArgs &a, 
         if (st + 2 < c.nst) ring_issue(c, smem, st + 2);
         if constexpr (FM > 0) {
             const float *sA = smem + (st % kRingSlots) * kSlotFloats, *sB = sA + kBK * 128;
-            ring_stage<FM>(sA, sB, am, bn, c.lane, acc);
+            ring_stage<FM, FN>(sA, sB, am, bn, c.lane, acc);
         }
     }
     // everyone is done with the ring before it becomes epilogue staging
@@ -626,7 +634,10 @@ __device__ __forceinline__ void ring_body(const RingCtx &c, const BuildArgs &a, 
     }
 }
 
-template <int MODE>
+// FN = 4 B-fragments: 64-wide wave tiles, WG 128x128.  (48-wide tiles with
+// FN = 3, which avoid padding at W = 240/720, measured slower: 414 vs 372 us
+// at config 2 -- more workgroups re-read A and the B DMA/FLOP grows.)
+template <int FN, int MODE>
 __global__ __launch_bounds__(256) void build_f32_ring_kernel(BuildArgs a, int nwg_total) {
     __shared__ __attribute__((aligned(16))) float smem[kRingSlots * kSlotFloats];
     RingCtx c;
@@ -641,20 +652,20 @@ __global__ __launch_bounds__(256) void build_f32_ring_kernel(BuildArgs a, int nw
     const int b = row / a.H;
     c.h = row - b * a.H;
     c.D = a.D; c.H = a.H; c.W1 = a.W1; c.W2 = a.W2;
-    c.M0 = tm * 128; c.N0 = tn * 128;
+    c.M0 = tm * 128; c.N0 = tn * 32 * FN;
     c.nst = (a.D + kBK - 1) / kBK;
     const long long img1 = (long long)a.D * a.H * a.W1, img2 = (long long)a.D * a.H * a.W2;
     c.r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
     c.r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
-    const int am = (c.wave >> 1) * 64, bn = (c.wave & 1) * 64;   // wave tile in the WG tile
+    const int am = (c.wave >> 1) * 64, bn = (c.wave & 1) * 16 * FN;   // wave tile in the WG tile
     const int m0 = c.M0 + am, n0 = c.N0 + bn;
     const int rows = a.W1 - m0;
-    const bool active = rows > 0 && n0 < a.W2;                    // wave-uniform
-    if (!active) ring_body<0, MODE>(c, a, smem, row, am, bn);
-    else if (rows > 48) ring_body<4, MODE>(c, a, smem, row, am, bn);
-    else if (rows > 32) ring_body<3, MODE>(c, a, smem, row, am, bn);
-    else if (rows > 16) ring_body<2, MODE>(c, a, smem, row, am, bn);
-    else ring_body<1, MODE>(c, a, smem, row, am, bn);
+    const bool active = rows > 0 && n0 < a.W2;                         // wave-uniform
+    if (!active) ring_body<0, FN, MODE>(c, a, smem, row, am, bn);
+    else if (rows > 48) ring_body<4, FN, MODE>(c, a, smem, row, am, bn);
+    else if (rows > 32) ring_body<3, FN, MODE>(c, a, smem, row, am, bn);
+    else if (rows > 16) ring_body<2, FN, MODE>(c, a, smem, row, am, bn);
+    else ring_body<1, FN, MODE>(c, a, smem, row, am, bn);
 }
 
 template <bool VEC, int U, int MODE>
@@ -663,8 +674,10 @@ static void launch(const BuildArgs &a, unsigned nwg, hipStream_t s) {
 }
 
 template <int MODE>
-static void launch_ring(const BuildArgs &a, unsigned nwg, hipStream_t s) {
-    hipLaunchKernelGGL((build_f32_ring_kernel<MODE>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
+static void launch_ring(const BuildArgs &a, hipStream_t s) {
+    const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
+    if (nwg <= 0 || nwg > 0x7FFFFFFF) return;
+    hipLaunchKernelGGL((build_f32_ring_kernel<4, MODE>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg);
 }
 
 template <bool IN_BF16, bool ALIGNED>
@@ -711,13 +724,13 @@ hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
         rc::launch<false, 2, 0>(a, n, s);
     } else {
         switch (mode) {
-            case 2: rc::launch_ring<2>(a, n, s); break;
+            case 2: rc::launch_ring<2>(a, s); break;
             case 128: rc::launch<true, 2, 0>(a, n, s); break;      // direct-load kernel
             case 130: rc::launch<true, 2, 2>(a, n, s); break;
             case 131: rc::launch<true, 2, 3>(a, n, s); break;
             case 129: rc::launch<true, 2, 1>(a, n, s); break;
             case 192: rc::launch<true, 2, 64>(a, n, s); break;
-            default: rc::launch_ring<0>(a, n, s); break;
+            default: rc::launch_ring<0>(a, s); break;
         }
     }
     return hipGetLastError();

@@ -227,3 +227,73 @@ def test_lookup_large_p_vs_oracle(pyr_dt):
     ref = coracle.corr_lookup([t.reshape(P, -1).float().cpu().numpy() for t in pyr],
                               coords.numpy(), L, r)
     assert same(out, ref)
+
+
+EDGE_SHAPES = [
+    # B, D, H, W1, W2, L, r
+    (1, 1, 1, 1, 16, 4, 4),       # D = 1, a single pixel
+    (2, 3, 1, 5, 2, 1, 1),        # W2 = 2, one level
+    (1, 8, 5, 1, 64, 6, 3),       # W1 = 1, 7 pyramid buffers
+    (1, 64, 1, 129, 128, 7, 2),   # 8 buffers: 7 fused + 1 pool-kernel level
+    (3, 16, 2, 67, 67, 2, 5),     # odd everything, radius 5
+]
+
+
+@pytest.mark.parametrize("shape", EDGE_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_edge_shapes_vs_oracle(shape):
+    B, D, H, W1, W2, L, r = shape
+    g = torch.Generator().manual_seed(101 + sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    x = torch.rand(B, 1, H, W1, generator=g) * (W2 + 8) - 4
+    coords = torch.cat([x, torch.randn(B, 1, H, W1, generator=g)], 1)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=r)
+        out = blk(coords.to(DEV)).cpu().numpy()
+    got = pyr_np(blk)
+    ref = coracle.corr_pyramid(f1.numpy(), f2.numpy(), L)
+    assert [a.shape for a in got] == [a.shape for a in ref]
+    assert norm_err(got[0], ref[0]) <= VOL_TOL
+    for i in range(L):
+        assert same(got[i + 1], coracle.corr_pool(got[i]))
+    assert same(out, coracle.corr_lookup(got[:L], coords.numpy(), L, r))
+
+
+def test_empty_inputs():
+    """B = 0 / H = 0: empty outputs of the right shapes, nothing launched."""
+    for B, H in ((0, 3), (2, 0)):
+        f = torch.randn(B, 8, H, 16, device=DEV)
+        blk = CorrBlock1D(f, f, num_levels=2, radius=2)
+        assert [t.shape for t in blk.corr_pyramid] == [(0, 1, 1, 16), (0, 1, 1, 8), (0, 1, 1, 4)]
+        out = blk(torch.zeros(B, 2, H, 16, device=DEV))
+        assert out.shape == (B, 10, H, 16)
+
+
+def test_noncontiguous_coords_and_fmaps():
+    """Strided coords (e.g. a view of a larger tensor) and non-contiguous fmaps
+    give the same result as their contiguous copies."""
+    g = torch.Generator().manual_seed(5)
+    f1 = torch.randn(2, 32, 4, 48, generator=g).to(DEV)
+    f2 = torch.randn(2, 32, 48, 4, generator=g).to(DEV).transpose(2, 3)   # non-contiguous
+    big = torch.randn(2, 5, 4, 48, generator=g).to(DEV) * 10 + 20
+    coords = big[:, 1:3]                                                    # strided view
+    with torch.no_grad():
+        a = CorrBlock1D(f1, f2, num_levels=3, radius=3)(coords)
+        b = CorrBlock1D(f1, f2.contiguous(), num_levels=3, radius=3)(coords.contiguous())
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("r", [1, 2, 3, 4, 6, 8])
+def test_levels_radius_grid(L, r):
+    g = torch.Generator().manual_seed(L * 10 + r)
+    B, D, H, W1, W2 = 1, 16, 2, 40, 96
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    x = torch.rand(B, 1, H, W1, generator=g) * 110 - 7
+    coords = torch.cat([x, torch.zeros_like(x)], 1)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=r)
+        out = blk(coords.to(DEV)).cpu().numpy()
+    got = pyr_np(blk)
+    assert same(out, coracle.corr_lookup(got[:L], coords.numpy(), L, r))

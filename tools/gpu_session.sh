@@ -26,7 +26,7 @@ rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
 has test  && step pytest_gpu 600 python -m pytest tests -m gpu -q -rf
 has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has bench && step bench 600 python bench.py
-has ablate && step ablate 600 python tools/ablate.py --build-modes 0,2,128,130 --lookup-variants 0
+has ablate && step ablate 600 python tools/ablate.py --build-modes 0,4,2,6 --lookup-variants 0
 has ablatek && step ablate_kitti 600 python tools/ablate.py --config kitti --build-modes 0,2,1,3 --lookup-variants 0,1,3
 has configs && step bench_realtime 300 python bench.py --config realtime --no-cpu-baseline --steps 50 --warmup 5 && step bench_realtime_graph 300 python bench.py --config realtime --graph --no-cpu-baseline --steps 200 --warmup 10
 has configs && step bench_middlebury 300 python bench.py --config middlebury --no-cpu-baseline --steps 5 --warmup 2
@@ -46,5 +46,10 @@ if has pmc; then
         --output-format csv -d "$OUT/pmc_sq" -o s -- python3 tools/probe.py
     python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --out "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
     cat "$OUT/traffic.log"
+fi
+if has pmcsq; then
+    step pmc_sq2 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE \
+        --output-format csv -d "$OUT/pmc_sq2" -o s -- python3 tools/probe.py
+    python tools/pmc_sq.py "$OUT/pmc_sq2" > "$OUT/pmc_sq2.txt" 2>&1; cat "$OUT/pmc_sq2.txt"
 fi
 exit 0
