@@ -312,7 +312,7 @@ def main():
                        "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                        "frac": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
                        "traffic": traffic.get("build_bytes"), "algorithmic_bytes": vbytes,
-                       "kernel": "rc::build_f32_kernel", "avg_launch_us": build_ms * 1e3}
+                       "kernel": "rc::build_f32_ring_kernel<4,0>", "avg_launch_us": build_ms * 1e3}
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": lgbs / HBM_PEAK_GBS, "traffic": traffic.get("lookup_bytes"),

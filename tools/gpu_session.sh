@@ -33,7 +33,7 @@ has configs && step bench_middlebury 300 python bench.py --config middlebury --n
 has configs && step bench_kitti 300 python bench.py --config kitti --no-cpu-baseline --steps 10 --warmup 3
 if has prof; then
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace \
-        -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline
+        -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0
     find "$OUT/prof" -name "*stats*.csv" -exec sh -c 'echo "== $1"; cat "$1"' _ {} \; > "$OUT/kernel_stats.txt" 2>/dev/null
     head -c 3000 "$OUT/kernel_stats.txt"
 fi
