@@ -9,6 +9,8 @@
  *                   used for levels beyond the fused epilogue (and for A/B runs).
  *   rc_corr_lookup  replaces CorrBlock1D.__call__ + bilinear_sampler
  *                   (model.py:297-316 and :267-281).
+ *   rc_corr_lookup_conv  the lookup fused with BasicMotionEncoder.convc1 +
+ *                   ReLU (model.py:199, :206), SURVEY.md §8f rank 1.
  *
  * The reference has no FFI; its "operator API" is the duck-typed class bound
  * at model.py:366-367 and called at :376.  raft-stereo_amd/corr.py mirrors that
@@ -86,6 +88,18 @@ int rc_corr_lookup(const void *const *pyr, const int *widths, const long *pyr_ld
                    int pyr_dtype, int levels, int radius, const float *coords_x,
                    long coord_batch_stride, int B, int H, int W1, float *out,
                    void *stream);
+
+/* Lookup fused with the motion encoder's first conv (model.py:199, :206):
+ *   out[b][c][h][w] = act(bias[c] + sum_k weight[c][k] * corr[b][k][h][w]),
+ *   corr = the rc_corr_lookup result (k = level*(2r+1) + tap, never written),
+ *   weight: [cout][levels*(2r+1)] fp32 (a 1x1 Conv2d weight), bias: [cout] or
+ *   NULL, act = ReLU when relu != 0.  out: [B][cout][H][W1] fp32.
+ *   levels 2..4, radius 1..4. */
+int rc_corr_lookup_conv(const void *const *pyr, const int *widths, const long *pyr_ld,
+                        int pyr_dtype, int levels, int radius, const float *coords_x,
+                        long coord_batch_stride, int B, int H, int W1,
+                        const float *weight, const float *bias, int cout, int relu,
+                        float *out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,8 @@ SIGNATURES = {
     "rc_corr_pool": (_i, [_vp, _l, _vp, _l, _l, _i, _i, _vp]),
     "rc_corr_lookup": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i, _i,
                             _i, _vp, _l, _i, _i, _i, _vp, _vp]),
+    "rc_corr_lookup_conv": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i,
+                                 _i, _i, _vp, _l, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
 }
 
 _lib = None

@@ -133,6 +133,60 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True):
     return pyr
 
 
+def _check_coords(pyramid, coords):
+    _require_hip(coords, "coords")
+    if coords.dim() != 4 or coords.shape[1] < 1:
+        raise RuntimeError("CorrBlock1D: coords must be (B, 2, H, W1)")
+    if coords.dtype != torch.float32:
+        raise RuntimeError(
+            f"CorrBlock1D: coords dtype {coords.dtype} != float32 (grid_sample "
+            "requires the grid dtype to match the volume, model.py:275)")
+    B, _, H, W1 = coords.shape
+    if B * H * W1 != pyramid[0].shape[0]:
+        raise RuntimeError(
+            f"CorrBlock1D: coords {tuple(coords.shape)} do not match the volume's "
+            f"{pyramid[0].shape[0]} rows (view at model.py:312)")
+    if coords.device != pyramid[0].device:
+        raise RuntimeError("CorrBlock1D: coords and pyramid on different devices")
+    x = coords[:, 0]
+    if x.stride(2) != 1 or x.stride(1) != W1:
+        x = x.contiguous()
+    cbs = x.stride(0) if B > 1 else H * W1
+    return x, cbs
+
+
+def _level_args(pyramid, num_levels):
+    levels = [pyramid[i] for i in range(num_levels)]
+    levels = [t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous() for t in levels]
+    return (levels, _lib.ptr_array([t.data_ptr() for t in levels]),
+            _lib.int_array([t.shape[-1] for t in levels]),
+            _lib.long_array([_row_stride(t) for t in levels]), _dtype_code(levels[0].dtype))
+
+
+def lookup_convc1(pyramid, coords, num_levels, radius, weight, bias=None, relu=True):
+    """Lookup fused with a 1x1 conv (+ReLU): relu(conv1x1(lookup(coords))),
+    i.e. BasicMotionEncoder's ``F.relu(self.convc1(corr))`` (model.py:199, :206)."""
+    x, cbs = _check_coords(pyramid, coords)
+    B, _, H, W1 = coords.shape
+    cin = num_levels * (2 * radius + 1)
+    w = weight.detach().reshape(weight.shape[0], -1).float().contiguous()
+    if w.shape[1] != cin:
+        raise RuntimeError(f"lookup_convc1: weight has {w.shape[1]} input channels, lookup gives {cin}")
+    b = bias.detach().float().contiguous() if bias is not None else None
+    cout = w.shape[0]
+    out = torch.empty((B, cout, H, W1), dtype=torch.float32, device=coords.device)
+    if B * H * W1 == 0:
+        return out
+    keep, ptrs, widths, lds, dt = _level_args(pyramid, num_levels)
+    with torch.cuda.device(coords.device):
+        rc = _lib.lib().rc_corr_lookup_conv(
+            ptrs, widths, lds, dt, num_levels, radius, x.data_ptr(), cbs, B, H, W1,
+            w.data_ptr(), b.data_ptr() if b is not None else None, cout, int(relu),
+            out.data_ptr(), _stream(coords.device))
+    _lib.check(rc, "rc_corr_lookup_conv")
+    return out
+
+
 def lookup(pyramid, coords, num_levels, radius):
     """Run rc_corr_lookup on levels [0, num_levels) of ``pyramid``."""
     _require_hip(coords, "coords")
@@ -186,6 +240,13 @@ class CorrBlock1D:
 
     def __call__(self, coords):
         return lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
+
+    def lookup_convc1(self, coords, weight, bias=None, relu=True):
+        """``relu(convc1(self(coords)))`` in one launch:
+        the motion encoder's first layer (model.py:199, :206) fused into the
+        lookup, so the (B, L(2r+1), H, W1) correlation never reaches HBM."""
+        return lookup_convc1(self.corr_pyramid, coords, self.num_levels, self.radius, weight,
+                             bias, relu)
 
     @staticmethod
     def corr(fmap1, fmap2):

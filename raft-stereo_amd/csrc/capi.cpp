@@ -120,44 +120,83 @@ extern "C" int rc_corr_pool(const void *in, long ld_in, void *out, long ld_out, 
                   "rc_corr_pool: launch");
 }
 
+namespace {
+// Shared validation of the lookup entry points; fills `a` or returns an error.
+int prep_lookup(const char *who, const void *const *pyr, const int *widths, const long *pyr_ld,
+                int pyr_dtype, int levels, int radius, const float *coords_x,
+                long coord_batch_stride, int B, int H, int W1, const float *out, rc::LookupArgs &a,
+                bool *empty) {
+    *empty = false;
+    if (levels < 1 || levels > RC_MAX_LEVELS)
+        return fail(RC_EINVAL, "%s: levels=%d outside 1..%d", who, levels, RC_MAX_LEVELS);
+    if (radius < 1 || radius > 8)
+        return fail(RC_EUNSUPPORTED, "%s: radius=%d outside 1..8", who, radius);
+    if (pyr_dtype != RC_F32 && pyr_dtype != RC_BF16)
+        return fail(RC_EINVAL, "%s: unknown pyramid dtype %d", who, pyr_dtype);
+    if (B < 0 || H < 0 || W1 < 0)
+        return fail(RC_EINVAL, "%s: bad shape B=%d H=%d W1=%d", who, B, H, W1);
+    if (!pyr || !widths) return fail(RC_EINVAL, "%s: null pyramid/width array", who);
+    const long long P = (long long)B * H * W1;
+    if (P == 0) {
+        *empty = true;
+        return RC_OK;
+    }
+    if ((long long)H * W1 > 0x7FFFFFFF) return fail(RC_EUNSUPPORTED, "%s: H*W1 too large", who);
+    if (!coords_x || !out) return fail(RC_EINVAL, "%s: null coords/out", who);
+    a = rc::LookupArgs{};
+    for (int i = 0; i < levels; ++i) {
+        if (widths[i] < 1) return fail(RC_EINVAL, "%s: level %d width %d", who, i, widths[i]);
+        if (!pyr[i] || !aligned16(pyr[i]))
+            return fail(RC_EINVAL, "%s: level %d null or not 16-byte aligned", who, i);
+        a.lvl[i] = pyr[i];
+        a.W[i] = widths[i];
+        a.ld[i] = pyr_ld ? pyr_ld[i] : widths[i];
+        if (a.ld[i] < widths[i])
+            return fail(RC_EINVAL, "%s: level %d row stride %lld < width %d", who, i, a.ld[i],
+                        widths[i]);
+    }
+    a.coords = coords_x;
+    a.cbs = coord_batch_stride;
+    a.P = P;
+    a.HW = H * W1;
+    a.levels = levels;
+    return RC_OK;
+}
+}  // namespace
+
 extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, const long *pyr_ld,
                               int pyr_dtype, int levels, int radius, const float *coords_x,
                               long coord_batch_stride, int B, int H, int W1, float *out,
                               void *stream) {
     g_err[0] = 0;
-    if (levels < 1 || levels > RC_MAX_LEVELS)
-        return fail(RC_EINVAL, "rc_corr_lookup: levels=%d outside 1..%d", levels, RC_MAX_LEVELS);
-    if (radius < 1 || radius > 8)
-        return fail(RC_EUNSUPPORTED, "rc_corr_lookup: radius=%d outside 1..8", radius);
-    if (pyr_dtype != RC_F32 && pyr_dtype != RC_BF16)
-        return fail(RC_EINVAL, "rc_corr_lookup: unknown pyramid dtype %d", pyr_dtype);
-    if (B < 0 || H < 0 || W1 < 0)
-        return fail(RC_EINVAL, "rc_corr_lookup: bad shape B=%d H=%d W1=%d", B, H, W1);
-    if (!pyr || !widths) return fail(RC_EINVAL, "rc_corr_lookup: null pyramid/width array");
-    const long long P = (long long)B * H * W1;
-    if (P == 0) return RC_OK;
-    if ((long long)H * W1 > 0x7FFFFFFF)
-        return fail(RC_EUNSUPPORTED, "rc_corr_lookup: H*W1 too large");
-    if (!coords_x || !out) return fail(RC_EINVAL, "rc_corr_lookup: null coords/out");
-    rc::LookupArgs a{};
-    for (int i = 0; i < levels; ++i) {
-        if (widths[i] < 1) return fail(RC_EINVAL, "rc_corr_lookup: level %d width %d", i, widths[i]);
-        if (!pyr[i] || !aligned16(pyr[i]))
-            return fail(RC_EINVAL, "rc_corr_lookup: level %d null or not 16-byte aligned", i);
-        a.lvl[i] = pyr[i];
-        a.W[i] = widths[i];
-        a.ld[i] = pyr_ld ? pyr_ld[i] : widths[i];
-        if (a.ld[i] < widths[i])
-            return fail(RC_EINVAL, "rc_corr_lookup: level %d row stride %lld < width %d", i, a.ld[i],
-                        widths[i]);
-    }
-    a.coords = coords_x;
-    a.cbs = coord_batch_stride;
+    rc::LookupArgs a;
+    bool empty;
+    int rc = prep_lookup("rc_corr_lookup", pyr, widths, pyr_ld, pyr_dtype, levels, radius, coords_x,
+                         coord_batch_stride, B, H, W1, out, a, &empty);
+    if (rc || empty) return rc;
     a.out = out;
-    a.P = P;
-    a.HW = H * W1;
-    a.levels = levels;
     return hip_rc(rc_launch_lookup(a, radius, pyr_dtype == RC_BF16,
                                    reinterpret_cast<hipStream_t>(stream)),
                   "rc_corr_lookup: launch");
+}
+
+extern "C" int rc_corr_lookup_conv(const void *const *pyr, const int *widths, const long *pyr_ld,
+                                   int pyr_dtype, int levels, int radius, const float *coords_x,
+                                   long coord_batch_stride, int B, int H, int W1,
+                                   const float *weight, const float *bias, int cout, int relu,
+                                   float *out, void *stream) {
+    g_err[0] = 0;
+    rc::LookupArgs a;
+    bool empty;
+    int rc = prep_lookup("rc_corr_lookup_conv", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
+                         coords_x, coord_batch_stride, B, H, W1, out, a, &empty);
+    if (rc) return rc;
+    if (levels < 2 || levels > 4 || radius > 4)
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_conv: levels 2..4 and radius 1..4 only");
+    if (cout < 1) return fail(RC_EINVAL, "rc_corr_lookup_conv: cout=%d", cout);
+    if (empty) return RC_OK;
+    if (!weight) return fail(RC_EINVAL, "rc_corr_lookup_conv: null weight");
+    return hip_rc(rc_launch_lookup_conv(a, radius, pyr_dtype == RC_BF16, weight, bias, cout, relu,
+                                        out, reinterpret_cast<hipStream_t>(stream)),
+                  "rc_corr_lookup_conv: launch");
 }

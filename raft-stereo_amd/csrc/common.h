@@ -74,3 +74,5 @@ hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStrea
 hipError_t rc_launch_pool(const void *in, long long ld_in, void *out, long long ld_out, long rows,
                           int W_in, int bf16, hipStream_t s);
 hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s);
+hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf16, const float *w,
+                                 const float *b, int cout, int relu, float *out, hipStream_t s);

@@ -85,10 +85,9 @@ __device__ __forceinline__ void issue_level(LevelWindow<R, BF16> &lw, const Look
     }
 }
 
-template <int R, bool BF16>
+template <int R, bool BF16, class Sink>
 __device__ __forceinline__ void finish_level(const LevelWindow<R, BF16> &lw, const LookupArgs &a,
-                                             int i, long long pblk, long long lrow, float *outp,
-                                             bool active) {
+                                             int i, long long pblk, long long lrow, Sink &&sink) {
     typedef LevelWindow<R, BF16> LW;
     constexpr int T = LW::T, NW = LW::NW, EPV = LW::EPV, NE = LW::NV * EPV;
     const int W = a.W[i];
@@ -143,7 +142,7 @@ __device__ __forceinline__ void finish_level(const LevelWindow<R, BF16> &lw, con
         const float v0 = ok0 ? a0 : 0.0f;
         const float v1 = ok1 ? a1 : 0.0f;
         const float res = fmaf(w1, v1, w0 * v0);
-        if (active) outp[(long long)(i * T + t) * a.HW] = res;
+        sink(t, res);
     }
 }
 
@@ -166,14 +165,75 @@ __global__ __launch_bounds__(BS) void lookup_kernel(LookupArgs a) {
 #pragma unroll
         for (int i = 0; i < NL; ++i) issue_level<R, BF16, EXACT>(lw[i], a, i, x, pblk, lrow);
 #pragma unroll
-        for (int i = 0; i < NL; ++i) finish_level<R, BF16>(lw[i], a, i, pblk, lrow, outp, active);
+        for (int i = 0; i < NL; ++i)
+            finish_level<R, BF16>(lw[i], a, i, pblk, lrow, [&](int t, float v) {
+                if (active) outp[(long long)(i * T + t) * a.HW] = v;
+            });
     } else {
         for (int i = 0; i < L; ++i) {
             LevelWindow<R, BF16> lw;
             issue_level<R, BF16, EXACT>(lw, a, i, x, pblk, lrow);
-            finish_level<R, BF16>(lw, a, i, pblk, lrow, outp, active);
+            finish_level<R, BF16>(lw, a, i, pblk, lrow, [&](int t, float v) {
+                if (active) outp[(long long)(i * T + t) * a.HW] = v;
+            });
         }
     }
+}
+
+// ---- lookup fused with the motion encoder's convc1 (+ ReLU) ----
+// BasicMotionEncoder.convc1 (model.py:199, :206) is a 1x1 conv over the
+// lookup's NL*(2r+1) channels: out[c] = relu(bias[c] + sum_k W[c][k] corr[k]).
+// The lane keeps its pixel's corr values in registers (levels unrolled, so
+// every index is static) and never writes them; the weights are read with
+// wave-uniform addresses (scalar loads).  Summation order: bias, then k
+// ascending, one fmaf each.
+template <int R, int NL, bool BF16>
+__global__ __launch_bounds__(256) void lookup_conv_kernel(LookupArgs a, const float *__restrict__ wgt,
+                                                          const float *__restrict__ bias, int cout,
+                                                          int relu, float *__restrict__ out) {
+    constexpr int T = 2 * R + 1, CIN = NL * T;
+    const long long pblk = (long long)blockIdx.x * 256;
+    const long long p = pblk + threadIdx.x;
+    const bool active = p < a.P;
+    const long long pp = active ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    const float x = a.coords[bimg * a.cbs + rem];
+    const long long lrow = pp - pblk;
+    float corr[CIN];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        LevelWindow<R, BF16> lw;
+        issue_level<R, BF16, true>(lw, a, i, x, pblk, lrow);
+        finish_level<R, BF16>(lw, a, i, pblk, lrow, [&](int t, float v) { corr[i * T + t] = v; });
+    }
+    float *op = out + bimg * (long long)cout * a.HW + rem;
+    for (int c = 0; c < cout; ++c) {
+        const float *wr = wgt + c * CIN;
+        float acc = bias ? bias[c] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < CIN; ++k) acc = fmaf(wr[k], corr[k], acc);
+        if (relu) acc = fmaxf(acc, 0.0f);
+        if (active) op[(long long)c * a.HW] = acc;
+    }
+}
+
+template <int R>
+static hipError_t launch_conv_r(const LookupArgs &a, int bf16, const float *w, const float *b,
+                                int cout, int relu, float *out, hipStream_t s) {
+    const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    if (a.levels == 4) {
+        if (bf16) hipLaunchKernelGGL((lookup_conv_kernel<R, 4, true>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
+        else hipLaunchKernelGGL((lookup_conv_kernel<R, 4, false>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
+    } else if (a.levels == 3) {
+        if (bf16) hipLaunchKernelGGL((lookup_conv_kernel<R, 3, true>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
+        else hipLaunchKernelGGL((lookup_conv_kernel<R, 3, false>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
+    } else if (a.levels == 2) {
+        if (bf16) hipLaunchKernelGGL((lookup_conv_kernel<R, 2, true>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
+        else hipLaunchKernelGGL((lookup_conv_kernel<R, 2, false>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 template <int R, int NL, bool BF16, bool EXACT, int BS = 256>
@@ -230,6 +290,18 @@ hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, h
         case 6: return rc::launch_r<6>(a, pyr_bf16, variant, s);
         case 7: return rc::launch_r<7>(a, pyr_bf16, variant, s);
         case 8: return rc::launch_r<8>(a, pyr_bf16, variant, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf16, const float *w,
+                                 const float *b, int cout, int relu, float *out, hipStream_t s) {
+    if (a.P <= 0) return hipSuccess;
+    switch (radius) {
+        case 1: return rc::launch_conv_r<1>(a, pyr_bf16, w, b, cout, relu, out, s);
+        case 2: return rc::launch_conv_r<2>(a, pyr_bf16, w, b, cout, relu, out, s);
+        case 3: return rc::launch_conv_r<3>(a, pyr_bf16, w, b, cout, relu, out, s);
+        case 4: return rc::launch_conv_r<4>(a, pyr_bf16, w, b, cout, relu, out, s);
         default: return hipErrorInvalidValue;
     }
 }

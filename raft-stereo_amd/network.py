@@ -177,8 +177,11 @@ class BasicMotionEncoder(nn.Module):
         self.convf2 = nn.Conv2d(64, 64, 3, padding=1)
         self.conv = nn.Conv2d(128, 126, 3, padding=1)
 
-    def forward(self, flow, corr):
-        c = F.relu(self.convc2(F.relu(self.convc1(corr))))
+    def forward(self, flow, corr, corr_is_convc1=False):
+        # corr_is_convc1: ``corr`` already is relu(convc1(corr)) (the fused
+        # lookup, CorrBlock1D.lookup_convc1)
+        c1 = corr if corr_is_convc1 else F.relu(self.convc1(corr))
+        c = F.relu(self.convc2(c1))
         f = F.relu(self.convf2(F.relu(self.convf1(flow))))
         return torch.cat([F.relu(self.conv(torch.cat([c, f], dim=1))), flow], dim=1)
 
@@ -211,7 +214,7 @@ class BasicMultiUpdateBlock(nn.Module):
                                   nn.Conv2d(256, (factor ** 2) * 9, 1, padding=0))
 
     def forward(self, net, inp, corr=None, flow=None, iter08=True, iter16=True, iter32=True,
-                update=True):
+                update=True, corr_is_convc1=False):
         n = self.args.n_gru_layers
         if iter32:
             net[2] = self.gru32(net[2], *inp[2], pool2x(net[1]))
@@ -219,7 +222,7 @@ class BasicMultiUpdateBlock(nn.Module):
             extra = (interp(net[2], net[1]),) if n > 2 else ()
             net[1] = self.gru16(net[1], *inp[1], pool2x(net[0]), *extra)
         if iter08:
-            motion = self.encoder(flow, corr)
+            motion = self.encoder(flow, corr, corr_is_convc1)
             extra = (interp(net[1], net[0]),) if n > 1 else ()
             net[0] = self.gru08(net[0], *inp[0], motion, *extra)
         if not update:
@@ -230,7 +233,7 @@ class BasicMultiUpdateBlock(nn.Module):
 class RAFTStereo(nn.Module):
     """model.py:335-383 with the correlation block pluggable (``corr_block``)."""
 
-    def __init__(self, args, corr_block=None):
+    def __init__(self, args, corr_block=None, fuse_convc1=False):
         super().__init__()
         self.args = args
         context_dims = args.hidden_dims
@@ -243,6 +246,8 @@ class RAFTStereo(nn.Module):
         self.conv2 = nn.Sequential(ResidualBlock(128, 128, "instance", stride=1),
                                    nn.Conv2d(128, 256, 3, padding=1))
         self.corr_block = corr_block or CorrBlock1D
+        # run convc1 + ReLU inside the lookup launch
+        self.fuse_convc1 = fuse_convc1
 
     def initialize_flow(self, img):
         N, _, H, W = img.shape
@@ -275,10 +280,15 @@ class RAFTStereo(nn.Module):
         coords0, coords1 = self.initialize_flow(net_list[0])
         if flow_init is not None:
             coords1 = coords1 + flow_init
+        fused = self.fuse_convc1 and hasattr(corr_fn, "lookup_convc1")
+        enc = self.update_block.encoder
         predictions = []
         for _ in range(iters):
             coords1 = coords1.detach()
-            corr = corr_fn(coords1)                     # the hot path, every iteration
+            if fused:                                   # lookup + convc1 + ReLU, one launch
+                corr = corr_fn.lookup_convc1(coords1, enc.convc1.weight, enc.convc1.bias)
+            else:
+                corr = corr_fn(coords1)                 # the hot path, every iteration
             flow = coords1 - coords0
             with self._autocast():
                 if a.n_gru_layers == 3 and a.slow_fast_gru:
@@ -289,7 +299,7 @@ class RAFTStereo(nn.Module):
                                                  iter16=True, iter08=False, update=False)
                 net_list, up_mask, delta_flow = self.update_block(
                     net_list, inp_list, corr, flow, iter32=a.n_gru_layers == 3,
-                    iter16=a.n_gru_layers >= 2)
+                    iter16=a.n_gru_layers >= 2, corr_is_convc1=fused)
             delta_flow[:, 1] = 0.0                       # D8 tail (see module docstring)
             coords1 = coords1 + delta_flow.float()
             predictions.append(coords1 - coords0)

@@ -297,3 +297,27 @@ def test_levels_radius_grid(L, r):
         out = blk(coords.to(DEV)).cpu().numpy()
     got = pyr_np(blk)
     assert same(out, coracle.corr_lookup(got[:L], coords.numpy(), L, r))
+
+
+@pytest.mark.parametrize("L,r,pyr_dt,bias,relu", [
+    (4, 4, torch.float32, True, True), (3, 4, torch.float32, True, True),
+    (2, 3, torch.float32, False, False), (4, 4, torch.bfloat16, True, True)])
+def test_lookup_convc1_vs_separate(L, r, pyr_dt, bias, relu):
+    """Fused lookup+convc1(+ReLU) vs our lookup followed by torch's 1x1 conv
+    (fp32).  Tolerance 1e-5 normalised: only the 1x1 conv's summation order
+    differs (k ascending fmaf chain vs the library's GEMM)."""
+    g = torch.Generator().manual_seed(31 * L + r)
+    B, D, H, W1, W2 = 2, 64, 5, 96, 96
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 30
+    coords = torch.cat([x, torch.zeros_like(x)], 1).to(DEV)
+    conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1, bias=bias).to(DEV)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=pyr_dt)
+        fused = blk.lookup_convc1(coords, conv.weight, conv.bias, relu=relu)
+        ref = conv(blk(coords))
+        if relu:
+            ref = torch.relu(ref)
+    assert fused.shape == ref.shape
+    assert norm_err(fused.cpu().numpy(), ref.cpu().numpy()) <= 1e-5

@@ -48,3 +48,19 @@ def test_bf16_autocast_runs():
     disp = flows[-1][:, 0].float().cpu().numpy()
     assert np.isfinite(disp).all()
     assert np.abs(disp - z["disparity"][-1]).mean() < 0.5
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_disparity_with_fused_convc1(name):
+    """The network with the lookup+convc1 fusion stays
+    within the north_star bar of the reference."""
+    case = CASES[name]
+    z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs(**case["args"]), fuse_convc1=True).eval().cuda()
+    with torch.no_grad():
+        flows = model(torch.from_numpy(z["image1"]).cuda(), torch.from_numpy(z["image2"]).cuda(),
+                      iters=int(z["iters"]))
+    disp = np.stack([f[:, 0].cpu().numpy() for f in flows], 0)
+    mae = np.abs(disp - z["disparity"]).mean(axis=(1, 2, 3))
+    assert (mae <= MAE_PX).all(), f"per-iteration MAE {mae}"

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--build-modes", default="0,32,8,4,2,1,3")
     ap.add_argument("--lookup-variants", default="0,1,3")
     ap.add_argument("--staggers", default="", help="RAFTCORR_STAGGER values to try with mode 64")
+    ap.add_argument("--convc1", action="store_true",
+                    help="also time lookup+convc1+relu fused vs separate (MIOpen 1x1 conv)")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
     B, D, H, W1, W2, L, r, iters, _ = cfg
@@ -79,6 +81,14 @@ def main():
                 os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
                 t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, coords[rnd % iters], L, r), 8)
                 res.setdefault(f"lookup_v{v}", []).extend(t)
+        if a.convc1:
+            conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1).to(dev)
+            for rnd in range(a.rounds):
+                c = coords[rnd % iters]
+                t = time_launches(lambda: ref_blk.lookup_convc1(c, conv.weight, conv.bias), 8)
+                res.setdefault("convc1_fused", []).extend(t)
+                t = time_launches(lambda: torch.relu(conv(ref_blk(c))), 8)
+                res.setdefault("convc1_separate", []).extend(t)
     out = {k: {"median_us": statistics.median(v), "min_us": min(v), "n": len(v)} for k, v in res.items()}
     print(json.dumps({"config": a.config, "results": out}, indent=1))
 
