@@ -148,8 +148,9 @@ __device__ __forceinline__ void finish_level(const LevelWindow<R, BF16> &lw, con
 
 // NL > 0: compile-time level count (all loads issue first); NL == 0: runtime.
 // BS = threads per block (256 for throughput, 64 to spread small problems).
-template <int R, int NL, bool BF16, bool EXACT, int BS = 256>
-__global__ __launch_bounds__(BS) void lookup_kernel(LookupArgs a) {
+template <int R, int NL, bool BF16, bool EXACT, int BS = 256, int WPE = 1>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE)))
+void lookup_kernel(LookupArgs a) {
     constexpr int T = 2 * R + 1;
     const long long pblk = (long long)blockIdx.x * BS;
     const long long p = pblk + threadIdx.x;
@@ -236,10 +237,10 @@ static hipError_t launch_conv_r(const LookupArgs &a, int bf16, const float *w, c
     return hipGetLastError();
 }
 
-template <int R, int NL, bool BF16, bool EXACT, int BS = 256>
+template <int R, int NL, bool BF16, bool EXACT, int BS = 256, int WPE = 1>
 static void launch_k(const LookupArgs &a, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + BS - 1) / BS);
-    hipLaunchKernelGGL((lookup_kernel<R, NL, BF16, EXACT, BS>), dim3(nblk), dim3(BS), 0, s, a);
+    hipLaunchKernelGGL((lookup_kernel<R, NL, BF16, EXACT, BS, WPE>), dim3(nblk), dim3(BS), 0, s, a);
 }
 
 // Below this many pixels the launch cannot fill the chip with the 256-thread
@@ -264,6 +265,9 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
     } else if (variant == 1) {
         if (bf16) launch_k<R, 0, true, false>(a, s);
         else launch_k<R, 0, false, false>(a, s);
+    } else if (variant == 4 && a.levels == 4) {
+        if (bf16) launch_k<R, 4, true, true, 256, 4>(a, s);
+        else launch_k<R, 4, false, true, 256, 4>(a, s);
     } else if (variant == 3 && a.levels == 4) {
         if (bf16) launch_k<R, 4, true, true>(a, s);
         else launch_k<R, 4, false, true>(a, s);
