@@ -155,6 +155,69 @@ def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False
             "note": "full network; encoders/GRU/heads on PyTorch (MIOpen) ops per north_star"}
 
 
+def backward_timing(cfg, f1, f2, coords, reps=3):
+    """Corr-path backward on the bench workload: per-kernel
+    event timing of rc_corr_lookup_backward (one per lookup call) and
+    rc_corr_build_backward, plus a whole autograd step (build + lookups +
+    backward through CorrBlock1D) with random output gradients."""
+    from raft_stereo_amd import corr as rcorr
+    B, D, H, W1, W2, L, r, iters, _ = cfg
+    P = B * H * W1
+    dev = f1.device
+    widths = [W2 >> i for i in range(L)]
+    g = torch.Generator().manual_seed(99)
+    gouts = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(2)]
+    grads = rcorr.grad_buffers(P, widths, dev)
+    for _ in range(2):   # warm-up
+        rcorr.lookup_backward(grads, coords[0], gouts[0], L, r)
+        rcorr.build_backward(f1, f2, grads)
+    lb, vb = [], []
+    for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 2)]
+        ev[0].record()
+        for it in range(iters):
+            rcorr.lookup_backward(grads, coords[it], gouts[it % 2], L, r)
+            ev[it + 1].record()
+        rcorr.build_backward(f1, f2, grads)
+        ev[iters + 1].record()
+        torch.cuda.synchronize()
+        lb += [ev[k].elapsed_time(ev[k + 1]) for k in range(iters)]
+        vb.append(ev[iters].elapsed_time(ev[iters + 1]))
+    lb_ms = sorted(lb)[len(lb) // 2]
+    vb_ms = sorted(vb)[len(vb) // 2]
+    # whole autograd step through the drop-in class
+    a = f1.detach().clone().requires_grad_(True)
+    b = f2.detach().clone().requires_grad_(True)
+
+    def train_step():
+        blk = CorrBlock1D(a, b, num_levels=L, radius=r)
+        outs = [blk(coords[it]) for it in range(iters)]
+        torch.autograd.backward(outs, [gouts[it % 2] for it in range(iters)])
+
+    train_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        train_step()
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / reps * 1e3
+    vflops = 2 * volume_flops(B, D, H, W1, W2)        # two GEMMs
+    lbytes = P * (4 + L * (2 * r + 1) * 4 + 2 * L * (2 * r + 2) * 4)   # x, grad_out, window RMW
+    return {"lookup_bwd_us": lb_ms * 1e3, "volume_bwd_us": vb_ms * 1e3,
+            "train_step_ms": step_ms, "train_pairs_per_s": B / (step_ms * 1e-3),
+            "roofline_volume_bwd": {"bound": "mfma", "achieved": vflops / (vb_ms * 1e-3) / 1e12,
+                                    "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                    "frac": vflops / (vb_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                                    "kernel": "rc::volume_bwd_kernel<true>"},
+            "roofline_lookup_bwd": {"bound": "hbm", "achieved": lbytes / (lb_ms * 1e-3) / 1e9,
+                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": lbytes / (lb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "algorithmic_bytes": lbytes,
+                                    "kernel": f"rc::lookup_bwd_kernel<{r}>"},
+            "note": "step = CorrBlock1D build + lookups + autograd backward to both fmaps "
+                    "(random output gradients); kernel times are medians of event-timed launches"}
+
+
 def load_traffic(path):
     try:
         with open(path) as fh:
@@ -177,6 +240,8 @@ def main():
                     help="also time the whole network this many steps (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    ap.add_argument("--no-backward", action="store_true",
+                    help="skip the corr-path backward timing (sceneflow only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -314,10 +379,12 @@ def main():
                        "traffic": traffic.get("build_bytes"), "algorithmic_bytes": vbytes,
                        "kernel": "rc::build_f32_ring_kernel<4,0>", "avg_launch_us": build_ms * 1e3}
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
+    lname = (f"rc::lookup_chain_kernel<{r},{L}>" if blk._chain
+             else f"rc::lookup_kernel<{r},0,{'true' if bf16 else 'false'},true>")
+    ltraffic = traffic.get("lookup_chain_bytes" if blk._chain else "lookup_bytes")
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": lgbs / HBM_PEAK_GBS, "traffic": traffic.get("lookup_bytes"),
-                   "algorithmic_bytes": lbytes,
-                   "kernel": f"rc::lookup_kernel<{r},0,{'true' if bf16 else 'false'},true>",
+                   "frac": lgbs / HBM_PEAK_GBS, "traffic": ltraffic,
+                   "algorithmic_bytes": lbytes, "kernel": lname,
                    "avg_launch_us": lookup_launch_ms * 1e3}
     dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
 
@@ -348,6 +415,8 @@ def main():
                       "lookup_per_launch": lookup_launch_ms},
         "cpu_baseline": None,
     }
+    if not args.no_backward and args.config == "sceneflow":
+        result["backward"] = backward_timing(cfg, f1, f2, coords)
     if args.e2e_steps > 0 and args.config == "sceneflow":
         result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1)
         result["e2e"]["pairs_per_s_all_ranks"] = result["e2e"]["pairs_per_s"] * world

@@ -11,6 +11,11 @@
  *                   (model.py:297-316 and :267-281).
  *   rc_corr_lookup_conv  the lookup fused with BasicMotionEncoder.convc1 +
  *                   ReLU (model.py:199, :206), SURVEY.md §8f rank 1.
+ *   rc_corr_lookup_chain  rc_corr_lookup for a pool-chain fp32 pyramid,
+ *                   reading levels 0-1 only (the default of CorrBlock1D).
+ *   rc_corr_lookup_backward, rc_corr_build_backward  the gradient of the
+ *                   path to the feature maps (autograd of model.py:267-326),
+ *                   SURVEY.md §8f rank 2.
  *
  * The reference has no FFI; its "operator API" is the duck-typed class bound
  * at model.py:366-367 and called at :376.  raft-stereo_amd/corr.py mirrors that
@@ -29,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 2
+#define RC_ABI_VERSION 3
 
 /* element types */
 #define RC_F32  0
@@ -100,6 +105,47 @@ int rc_corr_lookup_conv(const void *const *pyr, const int *widths, const long *p
                         long coord_batch_stride, int B, int H, int W1,
                         const float *weight, const float *bias, int cout, int relu,
                         float *out, void *stream);
+
+/* Lookup over a pool-chain fp32 pyramid (what rc_corr_build writes), same
+ * arguments and bit-identical results as rc_corr_lookup with RC_F32, but
+ * levels >= 2 are recomputed from level 1 (level l+1 = pairwise mean of level
+ * l, the fp32 ops of model.py:294), so only levels 0 and 1 are read: one
+ * level-1 span per pixel instead of one window per level.  Requires
+ * widths[i] == widths[i-1] / 2, pyr_ld[1] % 4 == 0, levels 3..4, radius
+ * 1..4.  pyr[i >= 2] are not read (the values must still be the pool chain
+ * for the results to equal rc_corr_lookup's). */
+int rc_corr_lookup_chain(const void *const *pyr, const int *widths, const long *pyr_ld,
+                         int levels, int radius, const float *coords_x,
+                         long coord_batch_stride, int B, int H, int W1, float *out,
+                         void *stream);
+
+/* Backward of rc_corr_lookup (model.py:297-316 through grid_sample's input
+ * gradient, :275): for every pixel p, level i and tap t, adds
+ * (x0+1-x')*g to grad_pyr[i][p][x0] and (x'-x0)*g to grad_pyr[i][p][x0+1]
+ * (zero-padded taps add nothing), g = grad_out[b][i*(2r+1)+t][h][w].
+ *   grad_pyr[i]: fp32, B*H*W1 rows of widths[i], row stride grad_ld[i]
+ *          (multiple of 4; NULL grad_ld = dense, then widths must be
+ *          multiples of 4), 16-byte aligned.  Accumulates: zero the buffers
+ *          once, then call once per lookup call.
+ *   grad_out: [B][levels*(2r+1)][H][W1] fp32 contiguous.  Other arguments as
+ *          rc_corr_lookup.  No atomics: pixel p owns row p. */
+int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long *grad_ld,
+                            int levels, int radius, const float *coords_x,
+                            long coord_batch_stride, int B, int H, int W1,
+                            const float *grad_out, void *stream);
+
+/* Backward of rc_corr_build (model.py:284-295 pooling, :318-326 volume):
+ *   Dl_{L-1} = grad_pyr[L-1], Dl_i[k] = grad_pyr[i][k] + Dl_{i+1}[k/2] / 2
+ *   (avg_pool2d's backward, floor widths), G = Dl_0 / sqrtf(D), and
+ *   grad_fmap1[b][d][h][w1] = sum_w2 G[b,h,w1,w2] * fmap2[b][d][h][w2]
+ *   grad_fmap2[b][d][h][w2] = sum_w1 G[b,h,w1,w2] * fmap1[b][d][h][w1]
+ *   (overwritten, fp32, exact-fp32 MFMA).  grad_pyr[l], l < levels: fp32
+ *   B*H*W1 rows of W2 >> l, row stride grad_ld[l] (grad_ld[0] % 4 == 0).
+ *   fmap_dtype RC_F32 only.  When B*H*W1 == 0 nothing is written. */
+int rc_corr_build_backward(const void *fmap1, const void *fmap2, int fmap_dtype,
+                           int B, int D, int H, int W1, int W2,
+                           const void *const *grad_pyr, const long *grad_ld, int levels,
+                           float *grad_fmap1, float *grad_fmap2, void *stream);
 
 #ifdef __cplusplus
 }

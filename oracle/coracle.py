@@ -33,6 +33,10 @@ def _load():
             ctypes.POINTER(_f32p), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
             ctypes.c_int, _f32p, ctypes.c_long, ctypes.c_int, ctypes.c_int,
             ctypes.c_int, _f32p]
+        lib.oracle_corr_lookup_backward.argtypes = lib.oracle_corr_lookup.argtypes
+        lib.oracle_corr_build_backward.argtypes = (
+            [_f32p, _f32p] + [ctypes.c_int] * 5 + [ctypes.POINTER(_f32p), ctypes.c_int,
+                                                   _f32p, _f32p, _f32p])
         _lib = lib
     return _lib
 
@@ -83,3 +87,44 @@ def corr_lookup(pyramid, coords, num_levels, radius):
     _load().oracle_corr_lookup(ptrs, widths, num_levels, radius, _p(coords),
                                2 * H * W1, B, H, W1, _p(out))
     return out
+
+
+def corr_lookup_backward(widths, coords, grad_out, num_levels, radius, grads=None):
+    """Accumulate the lookup's pyramid gradients: returns a list of (P, W_l)
+    (``grads`` to keep accumulating over several lookup calls)."""
+    coords = np.ascontiguousarray(coords, np.float32)
+    grad_out = np.ascontiguousarray(grad_out, np.float32)
+    B, _, H, W1 = coords.shape
+    P = B * H * W1
+    if grads is None:
+        grads = [np.zeros((P, widths[i]), np.float32) for i in range(num_levels)]
+    ptrs = (_f32p * num_levels)(*[_p(g) for g in grads])
+    wid = (ctypes.c_int * num_levels)(*widths[:num_levels])
+    _load().oracle_corr_lookup_backward(ptrs, wid, num_levels, radius, _p(coords), 2 * H * W1,
+                                        B, H, W1, _p(grad_out))
+    return grads
+
+
+def fold_grads(grads):
+    """Total gradient of every pyramid level: each level's own gradient plus
+    the pooling backward of the coarser total (model.py:294)."""
+    tot = [g.copy() for g in grads]
+    for i in range(len(grads) - 2, -1, -1):
+        Wc = tot[i + 1].shape[1]
+        tot[i][:, :2 * Wc] += np.repeat(tot[i + 1] * np.float32(0.5), 2, axis=1)
+    return tot
+
+
+def corr_build_backward(f1, f2, grads):
+    """(d fmap1, d fmap2) from the per-level pyramid gradients (fp64 GEMMs)."""
+    f1 = np.ascontiguousarray(f1, np.float32)
+    f2 = np.ascontiguousarray(f2, np.float32)
+    B, D, H, W1 = f1.shape
+    W2 = f2.shape[3]
+    grads = [np.ascontiguousarray(g, np.float32) for g in grads]
+    scratch = np.empty((B * H * W1, W2), np.float32)
+    df1, df2 = np.empty_like(f1), np.empty_like(f2)
+    ptrs = (_f32p * len(grads))(*[_p(g) for g in grads])
+    _load().oracle_corr_build_backward(_p(f1), _p(f2), B, D, H, W1, W2, ptrs, len(grads),
+                                       _p(scratch), _p(df1), _p(df2))
+    return df1, df2

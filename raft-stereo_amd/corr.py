@@ -11,9 +11,19 @@ so that ``RAFTStereo.forward`` can bind it where the reference does
       (:290-295; the last one is never read, as in the reference).  Rows whose
       width is not a 16-byte multiple are views into row-padded buffers
       (same shape and values, a larger row stride).
-  * ``__call__(coords)``  (model.py:297-316)  one rc_corr_lookup launch:
-      (B,2,H,W1) fp32 coords -> (B, num_levels*(2r+1), H, W1) fp32.
+  * ``__call__(coords)``  (model.py:297-316)  one lookup launch:
+      (B,2,H,W1) fp32 coords -> (B, num_levels*(2r+1), H, W1) fp32.  For an
+      fp32 pyramid with 3-4 levels it is rc_corr_lookup_chain, which reads
+      levels 0-1 only and recomputes the coarser ones (bit-identical to
+      rc_corr_lookup, fewer HBM lines per pixel); otherwise rc_corr_lookup.
   * ``CorrBlock1D.corr(fmap1, fmap2)``  (model.py:318-326) -> (B,H,W1,1,W2).
+  * Autograd: when an fmap requires grad, the lookups
+      and the build are autograd nodes.  Each lookup's backward adds its
+      grid_sample input gradient into level-gradient buffers shared by the
+      block (rc_corr_lookup_backward, no atomics); the build's backward,
+      which autograd runs after all of them, folds those through the pooling
+      backward and produces d fmap1 / d fmap2 with two fp32 MFMA GEMMs
+      (rc_corr_build_backward).  ``corr_pyramid`` itself carries no grad_fn.
 
 Error behaviour follows the reference where it has one: W2 < 2**num_levels
 raises RuntimeError (avg_pool2d, model.py:294); mismatched fmap shapes raise
@@ -22,8 +32,9 @@ RuntimeError (einsum, :324); coords that do not match the volume's
 RuntimeError (grid_sample dtype check, :275).
 
 Differences, all loud: tensors must live on a HIP device (no CPU fallback);
-the path is inference-only (asking for gradients raises); bf16/fp16 fmaps are
-accepted (the reference crashes on them): they, or
+the fused ``lookup_convc1`` is inference-only (asking for gradients raises);
+bf16/fp16 fmaps are accepted (the reference crashes on them, SURVEY.md
+Appendix A D9; their gradients are computed in fp32): they, or
 an explicit ``pyramid_dtype=torch.bfloat16``, select the bf16 MFMA kernel and
 a bf16 pyramid (bf16-level tolerance).
 """
@@ -70,10 +81,6 @@ def _check_fmaps(fmap1, fmap2):
             "disagree on (B, D, H) (einsum 'aijk,aijh->ajkh', model.py:324)")
     if fmap1.device != fmap2.device:
         raise RuntimeError("CorrBlock1D: fmaps on different devices")
-    if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
-        raise RuntimeError(
-            "raft_stereo_amd.CorrBlock1D is inference-only (backward is not "
-            "implemented); call it under torch.no_grad() or detach the fmaps")
     return B, D, H, W1, W2
 
 
@@ -189,41 +196,156 @@ def lookup_convc1(pyramid, coords, num_levels, radius, weight, bias=None, relu=T
 
 def lookup(pyramid, coords, num_levels, radius):
     """Run rc_corr_lookup on levels [0, num_levels) of ``pyramid``."""
-    _require_hip(coords, "coords")
-    if coords.dim() != 4 or coords.shape[1] < 1:
-        raise RuntimeError("CorrBlock1D: coords must be (B, 2, H, W1)")
-    if coords.dtype != torch.float32:
-        raise RuntimeError(
-            f"CorrBlock1D: coords dtype {coords.dtype} != float32 (grid_sample "
-            "requires the grid dtype to match the volume, model.py:275)")
+    x, cbs = _check_coords(pyramid, coords)
     B, _, H, W1 = coords.shape
-    P = pyramid[0].shape[0]
-    if B * H * W1 != P:
-        raise RuntimeError(
-            f"CorrBlock1D: coords {tuple(coords.shape)} do not match the volume's "
-            f"{P} rows (view at model.py:312)")
-    if coords.device != pyramid[0].device:
-        raise RuntimeError("CorrBlock1D: coords and pyramid on different devices")
-    x = coords[:, 0]
-    if x.stride(2) != 1 or x.stride(1) != W1:
-        x = x.contiguous()
-    cbs = x.stride(0) if B > 1 else H * W1
     C = num_levels * (2 * radius + 1)
     out = torch.empty((B, C, H, W1), dtype=torch.float32, device=coords.device)
-    if P == 0:
+    if B * H * W1 == 0:
         return out
-    levels = [pyramid[i] for i in range(num_levels)]
-    levels = [t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous() for t in levels]
-    dt = levels[0].dtype
+    keep, ptrs, widths, lds, dt = _level_args(pyramid, num_levels)
     with torch.cuda.device(coords.device):
-        rc = _lib.lib().rc_corr_lookup(
-            _lib.ptr_array([t.data_ptr() for t in levels]),
-            _lib.int_array([t.shape[-1] for t in levels]),
-            _lib.long_array([_row_stride(t) for t in levels]),
-            _dtype_code(dt), num_levels, radius, x.data_ptr(), cbs, B, H, W1,
-            out.data_ptr(), _stream(coords.device))
+        rc = _lib.lib().rc_corr_lookup(ptrs, widths, lds, dt, num_levels, radius, x.data_ptr(), cbs,
+                                       B, H, W1, out.data_ptr(), _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup")
     return out
+
+
+def chain_ok(pyramid, num_levels, radius):
+    """True when rc_corr_lookup_chain applies: an fp32 pool-chain pyramid with
+    3-4 levels, radius <= 4 and a 16-byte level-1 row stride."""
+    if num_levels not in (3, 4) or not 1 <= radius <= 4 or pyramid[0].dtype != torch.float32:
+        return False
+    if any(pyramid[i].shape[-1] != pyramid[i - 1].shape[-1] // 2 for i in range(1, num_levels)):
+        return False
+    lvl1 = pyramid[1]
+    return lvl1.stride(-1) == 1 and _row_stride(lvl1) % 4 == 0 and lvl1.data_ptr() % 16 == 0
+
+
+def lookup_chain(pyramid, coords, num_levels, radius):
+    """rc_corr_lookup_chain: same result as :func:`lookup` for a pyramid whose
+    levels are the avg-pool chain of level 0 (what :func:`build_pyramid`
+    writes), reading only levels 0 and 1 (include/raftcorr.h)."""
+    x, cbs = _check_coords(pyramid, coords)
+    B, _, H, W1 = coords.shape
+    out = torch.empty((B, num_levels * (2 * radius + 1), H, W1), dtype=torch.float32,
+                      device=coords.device)
+    if B * H * W1 == 0:
+        return out
+    keep, ptrs, widths, lds, dt = _level_args(pyramid, num_levels)
+    with torch.cuda.device(coords.device):
+        rc = _lib.lib().rc_corr_lookup_chain(ptrs, widths, lds, num_levels, radius, x.data_ptr(),
+                                             cbs, B, H, W1, out.data_ptr(), _stream(coords.device))
+    _lib.check(rc, "rc_corr_lookup_chain")
+    return out
+
+
+# ----------------------------------------------------------------- backward
+
+def grad_buffers(P, widths, device):
+    """Zeroed fp32 level-gradient buffers (P, W_l) with rows padded to 16 bytes
+    (the padding stays zero: rc_corr_lookup_backward never touches it)."""
+    bufs = []
+    for W in widths:
+        ld = -(-W // 4) * 4
+        bufs.append(torch.zeros((P, ld), dtype=torch.float32, device=device)[:, :W])
+    return bufs
+
+
+def lookup_backward(grads, coords, grad_out, num_levels, radius):
+    """rc_corr_lookup_backward: accumulate d(lookup)/d(level i) . grad_out into
+    ``grads`` (from :func:`grad_buffers`) -- grid_sample's input gradient
+    (model.py:275) for every level and tap of the lookup at ``coords``."""
+    x, cbs = _check_coords(grads, coords)
+    B, _, H, W1 = coords.shape
+    if B * H * W1 == 0:
+        return
+    go = grad_out.detach().float().contiguous()
+    if go.shape != (B, num_levels * (2 * radius + 1), H, W1):
+        raise RuntimeError(f"lookup_backward: grad_out shape {tuple(go.shape)}")
+    with torch.cuda.device(coords.device):
+        rc = _lib.lib().rc_corr_lookup_backward(
+            _lib.ptr_array([grads[i].data_ptr() for i in range(num_levels)]),
+            _lib.int_array([grads[i].shape[-1] for i in range(num_levels)]),
+            _lib.long_array([grads[i].stride(0) for i in range(num_levels)]),
+            num_levels, radius, x.data_ptr(), cbs, B, H, W1, go.data_ptr(),
+            _stream(coords.device))
+    _lib.check(rc, "rc_corr_lookup_backward")
+
+
+def build_backward(fmap1, fmap2, grads):
+    """rc_corr_build_backward: level gradients -> (d fmap1, d fmap2), fp32.
+    The pooling backward (model.py:294), the 1/sqrt(D) (:326) and the two
+    einsum operand gradients (:324) in one launch."""
+    f1 = fmap1.detach().float().contiguous()
+    f2 = fmap2.detach().float().contiguous()
+    B, D, H, W1 = f1.shape
+    W2 = f2.shape[3]
+    if B * H * W1 == 0:
+        return torch.zeros_like(f1), torch.zeros_like(f2)
+    df1, df2 = torch.empty_like(f1), torch.empty_like(f2)
+    with torch.cuda.device(f1.device):
+        rc = _lib.lib().rc_corr_build_backward(
+            f1.data_ptr(), f2.data_ptr(), _lib.RC_F32, B, D, H, W1, W2,
+            _lib.ptr_array([g.data_ptr() for g in grads]),
+            _lib.long_array([g.stride(0) for g in grads]), len(grads),
+            df1.data_ptr(), df2.data_ptr(), _stream(f1.device))
+    _lib.check(rc, "rc_corr_build_backward")
+    return df1, df2
+
+
+class _GradState:
+    """Level gradients shared by one CorrBlock1D's lookup nodes and its build
+    node.  Holds no pyramid and no graph node, so no reference cycle keeps the
+    pyramid alive."""
+
+    def __init__(self, P, widths, device, num_levels, radius):
+        self.P, self.widths, self.device = P, widths, device
+        self.num_levels, self.radius = num_levels, radius
+        self.grads = None
+
+    def accumulate(self, coords, grad_out):
+        if self.grads is None:
+            self.grads = grad_buffers(self.P, self.widths, self.device)
+        lookup_backward(self.grads, coords, grad_out, self.num_levels, self.radius)
+
+    def take(self):
+        g, self.grads = self.grads, None
+        return g
+
+
+class _BuildFn(torch.autograd.Function):
+    """Autograd node of the build.  Its output is a 0-d token every lookup
+    consumes, so autograd runs this backward after all of theirs; by then the
+    lookups have summed their level gradients into the shared state."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, state):
+        ctx.state = state
+        ctx.save_for_backward(fmap1, fmap2)
+        return torch.zeros((), dtype=torch.float32, device=fmap1.device)
+
+    @staticmethod
+    def backward(ctx, _token_grad):
+        f1, f2 = ctx.saved_tensors
+        grads = ctx.state.take()
+        if grads is None:          # no lookup output reached the loss
+            return None, None, None
+        df1, df2 = build_backward(f1, f2, grads)
+        return df1.to(f1.dtype), df2.to(f2.dtype), None
+
+
+class _LookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, token, coords, state, fn):
+        ctx.state = state
+        ctx.save_for_backward(coords)
+        return fn(coords)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (coords,) = ctx.saved_tensors
+        ctx.state.accumulate(coords, grad_out)
+        return torch.zeros((), dtype=torch.float32, device=coords.device), None, None, None
 
 
 class CorrBlock1D:
@@ -236,15 +358,37 @@ class CorrBlock1D:
             low = fmap1.dtype in (torch.bfloat16, torch.float16)
             pyramid_dtype = torch.bfloat16 if low else torch.float32
         self.pyramid_dtype = pyramid_dtype
-        self.corr_pyramid = build_pyramid(fmap1, fmap2, num_levels + 1, pyramid_dtype)
+        grad = torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad)
+        with torch.no_grad():
+            self.corr_pyramid = build_pyramid(fmap1, fmap2, num_levels + 1, pyramid_dtype)
+        # levels 0..L-1 are the pool chain of level 0 (the epilogue pools the
+        # stored values): the lookup reads levels 0 and 1 only
+        self._chain = chain_ok(self.corr_pyramid, num_levels, radius)
+        self._state = self._token = None
+        if grad:
+            B, _, H, W1 = fmap1.shape
+            self._state = _GradState(B * H * W1, [t.shape[-1] for t in self.corr_pyramid[:num_levels]],
+                                     fmap1.device, num_levels, radius)
+            self._token = _BuildFn.apply(fmap1, fmap2, self._state)
+
+    def _lookup(self, coords):
+        if self._chain:
+            return lookup_chain(self.corr_pyramid, coords, self.num_levels, self.radius)
+        return lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
 
     def __call__(self, coords):
-        return lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
+        if self._token is not None and torch.is_grad_enabled():
+            return _LookupFn.apply(self._token, coords.detach(), self._state, self._lookup)
+        return self._lookup(coords)
 
     def lookup_convc1(self, coords, weight, bias=None, relu=True):
         """``relu(convc1(self(coords)))`` in one launch:
         the motion encoder's first layer (model.py:199, :206) fused into the
-        lookup, so the (B, L(2r+1), H, W1) correlation never reaches HBM."""
+        lookup, so the (B, L(2r+1), H, W1) correlation never reaches HBM.
+        Inference only."""
+        if torch.is_grad_enabled() and (self._token is not None or weight.requires_grad):
+            raise RuntimeError("CorrBlock1D.lookup_convc1 is inference-only; use "
+                               "convc1(block(coords)) when gradients are needed")
         return lookup_convc1(self.corr_pyramid, coords, self.num_levels, self.radius, weight,
                              bias, relu)
 

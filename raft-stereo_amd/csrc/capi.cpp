@@ -180,6 +180,110 @@ extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, const l
                   "rc_corr_lookup: launch");
 }
 
+extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, const long *pyr_ld,
+                                    int levels, int radius, const float *coords_x,
+                                    long coord_batch_stride, int B, int H, int W1, float *out,
+                                    void *stream) {
+    g_err[0] = 0;
+    rc::LookupArgs a;
+    bool empty;
+    int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, RC_F32, levels, radius,
+                         coords_x, coord_batch_stride, B, H, W1, out, a, &empty);
+    if (rc) return rc;
+    if (levels < 3 || levels > 4 || radius > 4)
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: levels 3..4 and radius 1..4 only");
+    for (int i = 1; i < levels; ++i)
+        if (widths[i] != widths[i - 1] / 2)
+            return fail(RC_EINVAL, "rc_corr_lookup_chain: width %d of level %d is not floor(%d/2)",
+                        widths[i], i, widths[i - 1]);
+    if (empty) return RC_OK;
+    if (a.ld[1] % 4 != 0)
+        return fail(RC_EINVAL, "rc_corr_lookup_chain: level-1 row stride %lld is not a multiple of 4",
+                    a.ld[1]);
+    a.out = out;
+    return hip_rc(rc_launch_lookup_chain(a, radius, reinterpret_cast<hipStream_t>(stream)),
+                  "rc_corr_lookup_chain: launch");
+}
+
+extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
+                                       const long *grad_ld, int levels, int radius,
+                                       const float *coords_x, long coord_batch_stride, int B,
+                                       int H, int W1, const float *grad_out, void *stream) {
+    g_err[0] = 0;
+    rc::LookupArgs la;
+    bool empty;
+    int rc = prep_lookup("rc_corr_lookup_backward", grad_pyr, widths, grad_ld, RC_F32, levels,
+                         radius, coords_x, coord_batch_stride, B, H, W1, grad_out, la, &empty);
+    if (rc || empty) return rc;
+    rc::LookupBwdArgs a{};
+    for (int i = 0; i < levels; ++i) {
+        if (la.ld[i] % 4 != 0)
+            return fail(RC_EINVAL, "rc_corr_lookup_backward: row stride %lld of level %d is not a "
+                        "multiple of 4", la.ld[i], i);
+        a.g[i] = static_cast<float *>(const_cast<void *>(la.lvl[i]));
+        a.W[i] = la.W[i];
+        a.ld[i] = la.ld[i];
+    }
+    a.coords = coords_x;
+    a.cbs = coord_batch_stride;
+    a.grad_out = grad_out;
+    a.P = la.P;
+    a.HW = la.HW;
+    a.levels = levels;
+    return hip_rc(rc_launch_lookup_bwd(a, radius, reinterpret_cast<hipStream_t>(stream)),
+                  "rc_corr_lookup_backward: launch");
+}
+
+extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int fmap_dtype, int B,
+                                      int D, int H, int W1, int W2, const void *const *grad_pyr,
+                                      const long *grad_ld, int levels, float *grad_fmap1,
+                                      float *grad_fmap2, void *stream) {
+    g_err[0] = 0;
+    if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
+        return fail(RC_EINVAL, "rc_corr_build_backward: bad shape B=%d D=%d H=%d W1=%d W2=%d", B, D,
+                    H, W1, W2);
+    if (fmap_dtype != RC_F32)
+        return fail(RC_EUNSUPPORTED, "rc_corr_build_backward: fp32 feature maps only");
+    if (levels < 1 || levels > RC_MAX_LEVELS || (W2 >> (levels - 1)) < 1)
+        return fail(RC_EINVAL, "rc_corr_build_backward: levels=%d invalid for W2=%d", levels, W2);
+    if (!grad_pyr) return fail(RC_EINVAL, "rc_corr_build_backward: null gradient array");
+    if ((long long)B * H * W1 == 0) return RC_OK;   // nothing to reduce; outputs are empty
+    if (!fmap1 || !fmap2 || !grad_fmap1 || !grad_fmap2 || !aligned16(fmap1) || !aligned16(fmap2) ||
+        !aligned16(grad_fmap1) || !aligned16(grad_fmap2))
+        return fail(RC_EINVAL, "rc_corr_build_backward: feature maps and their gradients must be "
+                    "non-null and 16-byte aligned");
+    rc::BuildBwdArgs a{};
+    for (int l = 0; l < levels; ++l) {
+        const long ld = grad_ld ? grad_ld[l] : (long)(W2 >> l);
+        if (!grad_pyr[l] || !aligned16(grad_pyr[l]))
+            return fail(RC_EINVAL, "rc_corr_build_backward: level gradient %d null or not 16-byte "
+                        "aligned", l);
+        if (ld < (long)(W2 >> l))
+            return fail(RC_EINVAL, "rc_corr_build_backward: row stride %ld of level %d < width %d",
+                        ld, l, W2 >> l);
+        a.g[l] = static_cast<const float *>(grad_pyr[l]);
+        a.ld[l] = ld;
+        a.Wl[l] = W2 >> l;
+    }
+    if (a.ld[0] % 4 != 0)
+        return fail(RC_EINVAL, "rc_corr_build_backward: level-0 row stride %lld is not a multiple "
+                    "of 4", a.ld[0]);
+    a.nlev = levels;
+    a.f1 = static_cast<const float *>(fmap1);
+    a.f2 = static_cast<const float *>(fmap2);
+    a.df1 = grad_fmap1;
+    a.df2 = grad_fmap2;
+    a.B = B; a.D = D; a.H = H; a.W1 = W1; a.W2 = W2;
+    a.tm = (D + 127) / 128;
+    a.tn1 = (W1 + 127) / 128;
+    a.tn2 = (W2 + 127) / 128;
+    a.sq = std::sqrt((float)D);                 // :326 divides by sqrt(float(D))
+    a.pow2 = is_pow2_float(a.sq) ? 1 : 0;
+    a.scale = 1.0f / a.sq;
+    return hip_rc(rc_launch_volume_bwd(a, reinterpret_cast<hipStream_t>(stream)),
+                  "rc_corr_build_backward: launch");
+}
+
 extern "C" int rc_corr_lookup_conv(const void *const *pyr, const int *widths, const long *pyr_ld,
                                    int pyr_dtype, int levels, int radius, const float *coords_x,
                                    long coord_batch_stride, int B, int H, int W1,

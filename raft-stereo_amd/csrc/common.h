@@ -66,6 +66,33 @@ struct LookupArgs {
     int levels;
 };
 
+// Backward of the lookup: level gradients (fp32, row stride ld[i] % 4 == 0).
+struct LookupBwdArgs {
+    float *g[kMaxLevels];
+    int W[kMaxLevels];
+    long long ld[kMaxLevels];
+    const float *coords;
+    long long cbs;
+    const float *grad_out;    // [B][levels*(2r+1)][H][W1]
+    long long P;
+    int HW;
+    int levels;
+};
+
+// Backward of the build: level gradients -> feature-map gradients (fp32).
+struct BuildBwdArgs {
+    const float *f1, *f2;     // [B][D][H][W1], [B][D][H][W2]
+    const float *g[kMaxLevels];
+    long long ld[kMaxLevels]; // level-gradient row strides (ld[0] % 4 == 0)
+    int Wl[kMaxLevels];       // level widths W2 >> l
+    int nlev;
+    float *df1, *df2;         // outputs, layouts of f1 / f2
+    int B, D, H, W1, W2;
+    int tm, tn1, tn2;         // 128-row d tiles; 128-col tiles over W1 (dF1) / W2 (dF2)
+    float scale, sq;
+    int pow2;
+};
+
 }  // namespace rc
 
 // Host-side launchers (defined in the .hip files, called by capi.cpp).
@@ -76,3 +103,6 @@ hipError_t rc_launch_pool(const void *in, long long ld_in, void *out, long long 
 hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s);
 hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf16, const float *w,
                                  const float *b, int cout, int relu, float *out, hipStream_t s);
+hipError_t rc_launch_lookup_chain(const rc::LookupArgs &a, int radius, hipStream_t s);
+hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
+hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s);

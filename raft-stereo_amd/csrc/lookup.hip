@@ -28,6 +28,8 @@
 // coalesced along w1.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace rc {
@@ -66,19 +68,21 @@ __device__ __forceinline__ void issue_level(LevelWindow<R, BF16> &lw, const Look
     const long long e = lrow * ld + (long long)lw.n - (R + 1);
     const long long ea = e & ~(long long)(LW::EPV - 1);
     lw.sh = (int)(e - ea);
-    // exact span of elements the taps read (relative to the block base)
-    // (selects on floats first: a NaN/huge float must never reach an integer cast)
-    const float f0 = lw.inwin ? floorf(lw.xp[0]) : 0.0f;
-    const float f1 = lw.inwin ? floorf(lw.xp[LW::T - 1]) : 0.0f;
+    // exact span of elements the taps read, clipped to the row's [0, W): the
+    // zero padding masks everything outside (relative to the block base;
+    // selects on floats first: a NaN/huge float must never reach an integer cast)
+    const float f0 = lw.inwin ? fmaxf(floorf(lw.xp[0]), 0.0f) : 0.0f;
+    const float f1 = lw.inwin ? fminf(floorf(lw.xp[LW::T - 1]) + 1.0f, Wm1) : -1.0f;
+    const bool any = lw.inwin && f0 <= f1;
     const long long first = lrow * ld + (long long)f0;
-    const long long last = lrow * ld + (long long)f1 + 1;
+    const long long last = lrow * ld + (long long)f1;
     const char *base = reinterpret_cast<const char *>(a.lvl[i]) + pblk * ld * LW::ES;
     const auto rs = make_rsrc(base, clamp_bytes((a.P - pblk) * ld * LW::ES));
 #pragma unroll
     for (int k = 0; k < LW::NV; ++k) {
         const long long c0 = ea + (long long)k * LW::EPV;
         uint32_t off = (uint32_t)(c0 * LW::ES);
-        if (EXACT && !(lw.inwin && c0 <= last && c0 + LW::EPV - 1 >= first)) off = 0xFFFFFF00u;
+        if (EXACT && !(any && c0 <= last && c0 + LW::EPV - 1 >= first)) off = 0xFFFFFF00u;
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
 #pragma unroll
         for (int c = 0; c < 4; ++c) lw.q[k][c] = v[c];
@@ -179,6 +183,171 @@ void lookup_kernel(LookupArgs a) {
             });
         }
     }
+}
+
+// ---- lookup over a pool-chain pyramid: levels >= 2 derived from level 1 ----
+// When the levels are the avg_pool chain of level 0 -- the pyramid
+// rc_corr_build writes -- element j of level i >= 2 is the pairwise-mean tree
+// of level-1 elements [2^(i-1) j, 2^(i-1) (j+1)) evaluated in the same fp32
+// order as model.py:294 applied i-1 times, so it is recomputed from level 1
+// bit for bit.  The windows of levels 1..L-1 around x all lie inside ONE span
+// of level 1: the top level's 2r+4 window scaled by S = 2^(L-2) (48 elements
+// at L = 4, r = 4), starting at a multiple of S.  Reading that span once
+// (~2.1 128-B lines for its ~160-B exact part) replaces one ~1.3-line window
+// per level, so a pixel touches ~3.4 lines instead of ~4.9.
+// Level 0 keeps its own window.  fp32 pyramids only (a bf16 pyramid rounds
+// every level separately).
+
+template <int S>
+__device__ __forceinline__ float pool_tree(const float *v) {
+    if constexpr (S == 1) return v[0];
+    else return (pool_tree<S / 2>(v) + pool_tree<S / 2>(v + S / 2)) * 0.5f;
+}
+
+// level-i element k (S_i = 2^(i-1) level-1 elements) straight from memory
+template <int SI>
+__device__ __forceinline__ float derived_elem(const float *row1, long long k) {
+    float v[SI];
+#pragma unroll
+    for (int c = 0; c < SI; ++c) v[c] = row1[SI * k + c];
+    return pool_tree<SI>(v);
+}
+
+template <int R, int NL>
+__global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
+    static_assert(NL >= 3 && NL <= 4, "chain lookup: 3 or 4 levels");
+    constexpr int T = 2 * R + 1, NW = 2 * R + 4, TOP = NL - 1, S = 1 << (TOP - 1);
+    constexpr int NE1 = S * NW;                        // span elements of level 1
+    constexpr int SHM = (S % 4 == 0) ? 0 : 4 - S;      // max misalignment of its start
+    constexpr int NC1 = (NE1 + SHM + 3) / 4;           // 16-B chunks
+    const long long pblk = (long long)blockIdx.x * 256;
+    const long long p = pblk + threadIdx.x;
+    const bool active = p < a.P;
+    const long long pp = active ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    const float x = a.coords[bimg * a.cbs + rem];
+    float *outp = a.out + bimg * (long long)(NL * T) * a.HW + rem;
+    const long long lrow = pp - pblk;
+
+    // level 0: its own window (lookup_kernel's path)
+    LevelWindow<R, false> lw0;
+    issue_level<R, false, true>(lw0, a, 0, x, pblk, lrow);
+
+    // levels 1..TOP: one span of level 1, starting at e1 = S (n_top - R - 1)
+    const float xtop = x / (float)(1 << TOP);
+    const bool inwin = (xtop > -(float)(R + 4)) && (xtop < (float)(a.W[TOP] + R + 4));
+    const float ntop = inwin ? floorf(xtop) : 0.0f;
+    const int e1 = S * ((int)ntop - R - 1);
+    const int ea = e1 & ~3;
+    const int sh = e1 - ea;                            // 0 when S % 4 == 0
+    int lo = 0x7FFFFFFF, hi = -1;                      // union of the exact spans
+    if (inwin) {
+#pragma unroll
+        for (int i = 1; i <= TOP; ++i) {
+            const float Wm1 = (float)(a.W[i] - 1), half = Wm1 / 2.0f;
+            const float xl = x / (float)(1 << i);
+            const float xa = (float)(-R) + xl, xb = (float)R + xl;
+            const float pa = ((2.0f * xa) / Wm1 - 1.0f + 1.0f) * half;
+            const float pb = ((2.0f * xb) / Wm1 - 1.0f + 1.0f) * half;
+            const int f = max((int)floorf(pa), 0);
+            const int l = min((int)floorf(pb) + 1, a.W[i] - 1);
+            if (f <= l) {
+                lo = min(lo, f << (i - 1));
+                hi = max(hi, ((l + 1) << (i - 1)) - 1);
+            }
+        }
+    }
+    const long long ld1 = a.ld[1];
+    const float *lvl1 = static_cast<const float *>(a.lvl[1]);
+    const auto rs1 = make_rsrc(lvl1 + pblk * ld1, clamp_bytes((a.P - pblk) * ld1 * 4));
+    f32x4 q1[NC1];
+#pragma unroll
+    for (int k = 0; k < NC1; ++k) {
+        const int cs = ea + 4 * k;
+        const bool ok = cs <= hi && cs + 3 >= lo;      // lo >= 0 and hi < W_1: inside the row
+        q1[k] = ld4(rs1, ok ? (uint32_t)((lrow * ld1 + cs) * 4) : 0xFFFFFF00u);
+    }
+
+    // level 0 math + stores while the span is in flight
+    finish_level<R, false>(lw0, a, 0, pblk, lrow, [&](int t, float v) {
+        if (active) outp[(long long)t * a.HW] = v;
+    });
+
+    // s1[k] = level-1 element e1 + k
+    float s1[NE1];
+#pragma unroll
+    for (int k = 0; k < NE1; ++k) {
+        float r = q1[k >> 2][k & 3];
+#pragma unroll
+        for (int s = 1; s <= SHM; ++s)
+            if (k + s < 4 * NC1) r = (sh == s) ? q1[(k + s) >> 2][(k + s) & 3] : r;
+        s1[k] = r;
+    }
+    const float *row1 = lvl1 + pp * ld1;
+
+    auto level = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int SI = 1 << (i - 1), NDD = 1 << (TOP - i);
+        const int W = a.W[i];
+        const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+        const float xl = x / (float)(1 << i);
+        const float n = inwin ? floorf(xl) : 0.0f;
+        // n = NDD * n_top + dd, dd in [0, NDD) (x / 2^i is exact); a subnormal
+        // x can break that -- such a lane reads memory instead (valid = false)
+        const int dd = inwin ? (int)n - NDD * (int)ntop : 0;
+        const bool valid = inwin && dd >= 0 && dd < NDD;
+        // window element jj (level-i element n - R - 1 + jj) starts at level-1
+        // offset SI*(dd + jj) + (R+1)*(S - SI) of the span
+        float w[NW];
+#pragma unroll
+        for (int jj = 0; jj < NW; ++jj) {
+            float val = 0.0f;
+#pragma unroll
+            for (int d = 0; d < NDD; ++d) {
+                constexpr int base = (R + 1) * (S - SI);
+                const float v = pool_tree<SI>(s1 + base + SI * (d + jj));
+                val = (dd == d) ? v : val;
+            }
+            w[jj] = val;
+        }
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + xl;
+            const float xn = (2.0f * xt) / Wm1 - 1.0f;
+            const float xp = (xn + 1.0f) * half;
+            const float x0 = floorf(xp);
+            const float w1 = xp - x0, w0 = 1.0f - w1;
+            const float nt = n + (float)(t - R);
+            const bool lo_ = x0 < nt, hi_ = x0 > nt;
+            float a0 = lo_ ? w[t] : (hi_ ? w[t + 2] : w[t + 1]);
+            float a1 = lo_ ? w[t + 1] : (hi_ ? w[t + 3] : w[t + 2]);
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            if (__builtin_expect(inwin && (!valid || x0 < nt - 1.0f || x0 > nt + 1.0f), 0)) {
+                a0 = ok0 ? derived_elem<SI>(row1, (long long)x0) : 0.0f;
+                a1 = ok1 ? derived_elem<SI>(row1, (long long)x0 + 1) : 0.0f;
+            }
+            const float v0 = ok0 ? a0 : 0.0f;
+            const float v1 = ok1 ? a1 : 0.0f;
+            const float res = fmaf(w1, v1, w0 * v0);
+            if (active) outp[(long long)(i * T + t) * a.HW] = res;
+        }
+    };
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    if constexpr (TOP >= 3) level(std::integral_constant<int, 3>{});
+}
+
+template <int R>
+static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
+    const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    if (a.levels == 4)
+        hipLaunchKernelGGL((lookup_chain_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+    else if (a.levels == 3)
+        hipLaunchKernelGGL((lookup_chain_kernel<R, 3>), dim3(nblk), dim3(256), 0, s, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
 }
 
 // ---- lookup fused with the motion encoder's convc1 (+ ReLU) ----
@@ -294,6 +463,17 @@ hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, h
         case 6: return rc::launch_r<6>(a, pyr_bf16, variant, s);
         case 7: return rc::launch_r<7>(a, pyr_bf16, variant, s);
         case 8: return rc::launch_r<8>(a, pyr_bf16, variant, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t rc_launch_lookup_chain(const rc::LookupArgs &a, int radius, hipStream_t s) {
+    if (a.P <= 0) return hipSuccess;
+    switch (radius) {
+        case 1: return rc::launch_chain_r<1>(a, s);
+        case 2: return rc::launch_chain_r<2>(a, s);
+        case 3: return rc::launch_chain_r<3>(a, s);
+        case 4: return rc::launch_chain_r<4>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

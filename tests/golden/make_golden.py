@@ -122,6 +122,31 @@ def lookup_case(ref, name, B, D, H, W1, W2, L, r, seed, special=False):
             "nan_out": int(np.isnan(out.numpy()).sum())}
 
 
+def backward_case(ref, name, B, D, H, W1, W2, L, r, calls, seed):
+    """Autograd of the reference path: fmaps require grad, ``calls`` lookups at
+    different coordinates, loss = sum_k <out_k, G_k>.  Records the fmap
+    gradients and every read level's total gradient (retain_grad)."""
+    g = gen(seed)
+    f1 = torch.randn(B, D, H, W1, generator=g).requires_grad_(True)
+    f2 = torch.randn(B, D, H, W2, generator=g).requires_grad_(True)
+    blk = ref.CorrBlock1D(f1, f2, num_levels=L, radius=r)
+    for i in range(L):
+        blk.corr_pyramid[i].retain_grad()
+    coords = torch.stack([lookup_coords(B, H, W1, W2, g) for _ in range(calls)])
+    gouts = torch.randn(calls, B, L * (2 * r + 1), H, W1, generator=g)
+    loss = sum((blk(coords[k]) * gouts[k]).sum() for k in range(calls))
+    loss.backward()
+    d = {"fmap1": f1.detach().numpy(), "fmap2": f2.detach().numpy(), "coords": coords.numpy(),
+         "grad_out": gouts.numpy(), "grad_fmap1": f1.grad.numpy(), "grad_fmap2": f2.grad.numpy(),
+         "num_levels": np.int32(L), "radius": np.int32(r)}
+    for i in range(L):
+        lvl = blk.corr_pyramid[i]
+        d[f"grad_level{i}"] = lvl.grad.reshape(lvl.shape[0], -1).numpy()
+    np.savez_compressed(os.path.join(OUT, f"backward_{name}.npz"), **d)
+    return {"kind": "backward", "B": B, "D": D, "H": H, "W1": W1, "W2": W2, "L": L, "r": r,
+            "calls": calls}
+
+
 class Args:
     """The seven attributes model.py reads (SURVEY.md §5 'Config / flags')."""
     def __init__(self, **kw):
@@ -186,6 +211,10 @@ def main():
     cases["l_w60_L3"] = lookup_case(ref, "w60_L3", 2, 24, 2, 15, 60, 3, 4, 15)
     cases["l_special"] = lookup_case(ref, "special", 1, 16, 2, 16, 45, 4, 4, 16, special=True)
     cases["l_tiny"] = lookup_case(ref, "tiny", 1, 8, 2, 9, 16, 4, 2, 17)
+    cases["b_w37"] = backward_case(ref, "w37", 2, 16, 3, 37, 37, 4, 4, 3, 31)
+    cases["b_w64_L3"] = backward_case(ref, "w64_L3", 1, 32, 2, 40, 64, 3, 3, 2, 32)
+    cases["b_d256"] = backward_case(ref, "d256", 1, 256, 2, 24, 40, 4, 4, 2, 33)
+    cases["b_w45_L2"] = backward_case(ref, "w45_L2", 1, 8, 2, 16, 45, 2, 2, 3, 34)
     cases["e2e_default"] = e2e_case(ref, "default", 64, 96, 12, 21)
     cases["e2e_sfgru"] = e2e_case(ref, "sfgru", 64, 80, 6, 22, slow_fast_gru=True, corr_levels=3,
                                   corr_radius=3)

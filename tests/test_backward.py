@@ -1,0 +1,182 @@
+"""Backward of the correlation path.
+
+The reference path is differentiable to the feature maps (model.py:375
+detaches only the coordinates).  Goldens (tests/golden/backward_*.npz, made
+by make_golden.py with the reference's own autograd) hold the fmap gradients
+and every read level's total gradient for several lookup calls per block.
+
+Tolerances (fp32, the SURVEY §8d contract): max|d|/max|ref| <= 1e-4 and
+rel-L2 <= 1e-5 for the fmap gradients; level gradients <= 1e-5 normalised
+(the only difference is the summation order of tap / call contributions).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import files, load, norm_err, rel_l2
+from oracle import coracle
+
+BWD = files("backward")
+TOL, L2 = 1e-4, 1e-5
+
+
+def oracle_grads(z):
+    """Oracle backward for a golden case: per-level grads, folded totals,
+    fmap grads."""
+    L, r = int(z["num_levels"]), int(z["radius"])
+    W2 = z["fmap2"].shape[3]
+    widths = [W2 >> i for i in range(L)]
+    g = None
+    for k in range(z["coords"].shape[0]):
+        g = coracle.corr_lookup_backward(widths, z["coords"][k], z["grad_out"][k], L, r, g)
+    df1, df2 = coracle.corr_build_backward(z["fmap1"], z["fmap2"], g)
+    return g, coracle.fold_grads(g), df1, df2
+
+
+def test_backward_goldens_present():
+    assert len(BWD) >= 4
+
+
+@pytest.mark.parametrize("path", BWD, ids=lambda p: p.split("/")[-1])
+def test_oracle_backward_vs_reference(path):
+    """The C oracle restates the reference's autograd (CPU only)."""
+    z = load(path)
+    L = int(z["num_levels"])
+    _, tot, df1, df2 = oracle_grads(z)
+    for i in range(L):
+        assert norm_err(tot[i], z[f"grad_level{i}"]) <= 1e-5, f"level {i}"
+    assert norm_err(df1, z["grad_fmap1"]) <= 1e-5 and rel_l2(df1, z["grad_fmap1"]) <= 1e-6
+    assert norm_err(df2, z["grad_fmap2"]) <= 1e-5 and rel_l2(df2, z["grad_fmap2"]) <= 1e-6
+
+
+# ------------------------------------------------------------------ GPU
+
+DEV = "cuda:0"
+
+
+def cu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def run_autograd(f1, f2, coords_list, gout_list, L, r, pyramid_dtype=None):
+    """Our CorrBlock1D under autograd: returns (d fmap1, d fmap2)."""
+    from raft_stereo_amd import CorrBlock1D
+    a = f1.detach().clone().requires_grad_(True)
+    b = f2.detach().clone().requires_grad_(True)
+    blk = CorrBlock1D(a, b, num_levels=L, radius=r, pyramid_dtype=pyramid_dtype)
+    loss = sum((blk(c) * g).sum() for c, g in zip(coords_list, gout_list))
+    loss.backward()
+    return a.grad, b.grad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", BWD, ids=lambda p: p.split("/")[-1])
+def test_backward_vs_golden(path):
+    z = load(path)
+    L, r = int(z["num_levels"]), int(z["radius"])
+    n = z["coords"].shape[0]
+    d1, d2 = run_autograd(cu(z["fmap1"]), cu(z["fmap2"]), [cu(z["coords"][k]) for k in range(n)],
+                          [cu(z["grad_out"][k]) for k in range(n)], L, r)
+    d1, d2 = d1.cpu().numpy(), d2.cpu().numpy()
+    assert norm_err(d1, z["grad_fmap1"]) <= TOL and rel_l2(d1, z["grad_fmap1"]) <= L2
+    assert norm_err(d2, z["grad_fmap2"]) <= TOL and rel_l2(d2, z["grad_fmap2"]) <= L2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", BWD, ids=lambda p: p.split("/")[-1])
+def test_lookup_backward_levels_vs_oracle(path):
+    """rc_corr_lookup_backward alone: per-level gradients vs the oracle."""
+    from raft_stereo_amd import corr as rcorr
+    z = load(path)
+    L, r = int(z["num_levels"]), int(z["radius"])
+    g_ref, _, _, _ = oracle_grads(z)
+    B, _, H, W1 = z["coords"][0].shape
+    W2 = z["fmap2"].shape[3]
+    grads = rcorr.grad_buffers(B * H * W1, [W2 >> i for i in range(L)], torch.device(DEV))
+    for k in range(z["coords"].shape[0]):
+        rcorr.lookup_backward(grads, cu(z["coords"][k]), cu(z["grad_out"][k]), L, r)
+    for i in range(L):
+        got = grads[i].cpu().numpy()
+        assert norm_err(got, g_ref[i]) <= 1e-6, f"level {i}"
+        # the row padding is never written
+        full = torch.as_strided(grads[i], (grads[i].shape[0], grads[i].stride(0)),
+                                (grads[i].stride(0), 1))
+        assert torch.count_nonzero(full[:, grads[i].shape[1]:]) == 0
+
+
+SHAPES = [
+    # B, D, H, W1, W2, L, r, calls
+    (2, 256, 3, 240, 240, 4, 4, 3),     # config-2 row width
+    (1, 64, 2, 311, 311, 4, 4, 2),      # W % 4 != 0 (scalar paths)
+    (1, 37, 2, 33, 70, 3, 3, 2),        # D % 4 != 0, W1 != W2
+    (1, 200, 1, 130, 129, 5, 2, 2),     # D, W not multiples of 128; 5 levels
+    (3, 16, 1, 8, 16, 1, 1, 4),         # tiny, one level
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_backward_random_vs_oracle(shape):
+    B, D, H, W1, W2, L, r, calls = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    cs, gs = [], []
+    for _ in range(calls):
+        x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 48
+        x[..., ::5] = torch.randint(-12, W2 + 12, x[..., ::5].shape, generator=g).float()
+        cs.append(torch.cat([x, torch.randn(B, 1, H, W1, generator=g)], 1))
+        gs.append(torch.randn(B, L * (2 * r + 1), H, W1, generator=g))
+    d1, d2 = run_autograd(f1.to(DEV), f2.to(DEV), [c.to(DEV) for c in cs], [x.to(DEV) for x in gs],
+                          L, r)
+    widths = [W2 >> i for i in range(L)]
+    gr = None
+    for c, x in zip(cs, gs):
+        gr = coracle.corr_lookup_backward(widths, c.numpy(), x.numpy(), L, r, gr)
+    r1, r2 = coracle.corr_build_backward(f1.numpy(), f2.numpy(), gr)
+    d1, d2 = d1.cpu().numpy(), d2.cpu().numpy()
+    assert norm_err(d1, r1) <= TOL and rel_l2(d1, r1) <= L2
+    assert norm_err(d2, r2) <= TOL and rel_l2(d2, r2) <= L2
+
+
+@pytest.mark.gpu
+def test_backward_matches_torch_autograd_of_restatement():
+    """Same inputs through the reference's ATen sequence (oracle/torch_ref.py,
+    autograd on the GPU) and through our kernels."""
+    from oracle import torch_ref
+    g = torch.Generator().manual_seed(77)
+    B, D, H, W1, W2, L, r = 2, 64, 4, 96, 96, 4, 4
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 40
+    c = torch.cat([x, torch.zeros_like(x)], 1).to(DEV)
+    go = torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(DEV)
+    d1, d2 = run_autograd(f1, f2, [c], [go], L, r)
+    a = f1.clone().requires_grad_(True)
+    b = f2.clone().requires_grad_(True)
+    (torch_ref.TorchCorrBlock1D(a, b, L, r)(c) * go).sum().backward()
+    assert norm_err(d1.cpu().numpy(), a.grad.cpu().numpy()) <= TOL
+    assert norm_err(d2.cpu().numpy(), b.grad.cpu().numpy()) <= TOL
+
+
+@pytest.mark.gpu
+def test_backward_bf16_fmaps_and_unused_lookup():
+    """bf16 fmaps get bf16 gradients (computed in fp32); a block whose lookups
+    never reach the loss gives no gradient; inference is unaffected."""
+    from raft_stereo_amd import CorrBlock1D
+    g = torch.Generator().manual_seed(5)
+    f1 = torch.randn(1, 32, 2, 64, generator=g).to(DEV, torch.bfloat16).requires_grad_(True)
+    f2 = torch.randn(1, 32, 2, 64, generator=g).to(DEV, torch.bfloat16).requires_grad_(True)
+    c = (torch.arange(64).float().view(1, 1, 1, 64) - 10).expand(1, 2, 2, 64).contiguous().to(DEV)
+    blk = CorrBlock1D(f1, f2, num_levels=4, radius=4)
+    blk(c).sum().backward()
+    assert f1.grad.dtype == torch.bfloat16 and torch.isfinite(f1.grad.float()).all()
+    assert f2.grad.abs().sum() > 0
+    h1 = f1.detach().float().requires_grad_(True)
+    blk2 = CorrBlock1D(h1, h1.detach(), num_levels=2, radius=2)
+    blk2(c)                                     # output unused
+    (h1 * 0).sum().backward()
+    assert torch.count_nonzero(h1.grad) == 0
+    with torch.no_grad():
+        out = CorrBlock1D(h1, h1, num_levels=2, radius=2)(c)
+    assert out.grad_fn is None

@@ -149,8 +149,59 @@ def test_errors_mirror_reference():
     with pytest.raises(RuntimeError):
         blk(torch.zeros(1, 2, 2, 16, device=DEV, dtype=torch.float64))     # dtype
     fg = f.clone().requires_grad_(True)
+    conv = torch.nn.Conv2d(18, 8, 1).to(DEV)
     with pytest.raises(RuntimeError, match="inference-only"):
-        CorrBlock1D(fg, fg)
+        CorrBlock1D(fg, fg, num_levels=2, radius=4).lookup_convc1(
+            torch.zeros(1, 2, 2, 16, device=DEV), conv.weight, conv.bias)
+
+
+CHAIN_SHAPES = [
+    # B, D, H, W1, W2, L, r
+    (2, 64, 3, 240, 240, 4, 4),
+    (1, 32, 2, 311, 311, 4, 4),     # odd widths: 311/155/77/38
+    (1, 16, 3, 45, 45, 4, 3),
+    (1, 16, 2, 60, 61, 3, 4),       # 3 levels: span start at even offsets
+    (2, 8, 2, 33, 130, 3, 2),
+    (1, 8, 2, 20, 16, 4, 1),        # W2 = 16: level 3 of width 2
+]
+
+
+def special_coords(B, H, W1, W2, g):
+    x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 64
+    x[..., ::6] = torch.randint(-30, W2 + 30, x[..., ::6].shape, generator=g).float()
+    x[..., 1::9] = x[..., 1::9] / 7.0 - 3.0
+    flat = x.reshape(-1)
+    vals = [float("nan"), float("inf"), -float("inf"), 1e30, -1e30, 0.0, -0.0, 1e-45, -1e-45,
+            -2.8e-45, 3.0e-39, -3.0e-39, -1e-40, W2 - 1.0, W2 + 3.999, -4.5, -33.0, -35.0]
+    flat[:len(vals)] = torch.tensor(vals)
+    return torch.cat([flat.view(B, 1, H, W1), torch.zeros(B, 1, H, W1)], 1)
+
+
+@pytest.mark.parametrize("shape", CHAIN_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_chain_lookup_bitexact(shape):
+    """rc_corr_lookup_chain (levels >= 2 recomputed from level 1) == the
+    per-level lookup == the oracle, bit for bit, incl. NaN/inf/subnormal x."""
+    B, D, H, W1, W2, L, r = shape
+    g = torch.Generator().manual_seed(900 + sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    coords = special_coords(B, H, W1, W2, g)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        assert blk._chain
+        a = rcorr.lookup_chain(blk.corr_pyramid, coords.to(DEV), L, r).cpu().numpy()
+        b = rcorr.lookup(blk.corr_pyramid, coords.to(DEV), L, r).cpu().numpy()
+    assert same(a, b)
+    assert same(a, coracle.corr_lookup(pyr_np(blk)[:L], coords.numpy(), L, r))
+
+
+def test_chain_not_used_for_bf16_or_other_levels():
+    f = torch.randn(1, 8, 2, 64, device=DEV)
+    with torch.no_grad():
+        assert not CorrBlock1D(f, f, num_levels=4, pyramid_dtype=torch.bfloat16)._chain
+        assert not CorrBlock1D(f, f, num_levels=2)._chain
+        assert not CorrBlock1D(f, f, num_levels=5, radius=2)._chain
+        assert not CorrBlock1D(f, f, num_levels=4, radius=5)._chain
 
 
 def test_repeat_launches_deterministic():

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--build-modes", default="0,32,8,4,2,1,3")
     ap.add_argument("--lookup-variants", default="0,1,3")
     ap.add_argument("--staggers", default="", help="RAFTCORR_STAGGER values to try with mode 64")
+    ap.add_argument("--chain", action="store_true",
+                    help="time rc_corr_lookup_chain vs the per-level rc_corr_lookup")
     ap.add_argument("--convc1", action="store_true",
                     help="also time lookup+convc1+relu fused vs separate (MIOpen 1x1 conv)")
     a = ap.parse_args()
@@ -81,6 +83,13 @@ def main():
                 os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
                 t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, coords[rnd % iters], L, r), 8)
                 res.setdefault(f"lookup_v{v}", []).extend(t)
+        if a.chain:
+            for rnd in range(a.rounds):
+                c = coords[rnd % iters]
+                t = time_launches(lambda: rcorr.lookup_chain(ref_blk.corr_pyramid, c, L, r), 8)
+                res.setdefault("lookup_chain", []).extend(t)
+                t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, c, L, r), 8)
+                res.setdefault("lookup_perlevel", []).extend(t)
         if a.convc1:
             conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1).to(dev)
             for rnd in range(a.rounds):

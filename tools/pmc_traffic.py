@@ -55,7 +55,8 @@ def main():
     kf = GiB / (cal_f[0] * 1024) if cal_f else 2.0
     kw = GiB / (cal_w[0] * 1024) if cal_w else 1.0
     res = {}
-    for kname, key in (("build", "build_"), ("lookup", "lookup_kernel")):
+    for kname, key in (("build", "build_"), ("lookup", "lookup_kernel"),
+                       ("lookup_chain", "lookup_chain_kernel")):
         f = per_kernel(fr, key)
         w = per_kernel(wr, key)
         if f is None or w is None:

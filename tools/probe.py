@@ -3,8 +3,8 @@
     python tools/probe.py [--config sceneflow] [--iters N]
 
 Launches, in order: a calibration copy (torch clone of a 1 GiB fp32 tensor:
-exactly 1 GiB read + 1 GiB written), N builds (rc::build_f32_kernel) and N
-lookups (rc::lookup_kernel) of bench.py's workload.  tools/pmc_traffic.py turns
+exactly 1 GiB read + 1 GiB written), N builds (rc::build_f32_ring_kernel), N
+CorrBlock1D lookups (rc::lookup_chain_kernel) and N per-level lookups (rc::lookup_kernel) of bench.py's workload.  tools/pmc_traffic.py turns
 the per-dispatch FETCH_SIZE / WRITE_SIZE into bytes per launch.
 """
 import argparse
@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from raft_stereo_amd import CorrBlock1D  # noqa: E402
+from raft_stereo_amd import corr as rcorr  # noqa: E402
 
 
 def main():
@@ -38,7 +39,9 @@ def main():
         for _ in range(a.iters):
             blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=pdt)
         for it in range(a.iters):
-            blk(coords[it % iters])
+            blk(coords[it % iters])        # rc::lookup_chain_kernel (fp32) / lookup_kernel
+        for it in range(a.iters):          # the per-level kernel on the same pyramid
+            rcorr.lookup(blk.corr_pyramid, coords[it % iters], L, r)
         torch.cuda.synchronize()
     print("probe done")
 
