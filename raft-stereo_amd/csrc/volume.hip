@@ -581,9 +581,10 @@ struct RingCtx {
 
 // DMA share of this wave per stage: rows 4w..4w+3 of both tiles, 2 rows
 // (1 KB = 64 lanes x 16 B) per instruction -> 4 instructions per stage.
+template <int SL>
 __device__ __forceinline__ void ring_issue(const RingCtx &c, float *smem, int st) {
     typedef __attribute__((address_space(3))) void lds_void;
-    float *sA = smem + (st % kRingSlots) * kSlotFloats, *sB = sA + kBK * 128;
+    float *sA = smem + (st % SL) * kSlotFloats, *sB = sA + kBK * 128;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r0 = 4 * c.wave + 2 * i;
@@ -601,7 +602,7 @@ __device__ __forceinline__ void ring_issue(const RingCtx &c, float *smem, int st
 // B-fragments (FM = 0: a wave with no valid rows -- it still issues its DMA
 // share and joins every barrier, so all four waves execute the same barrier
 // sequence).
-template <int FM, int FN, int MODE>
+template <int FM, int FN, int MODE, int SL>
 __device__ __forceinline__ void ring_body(const RingCtx &c, const BuildArgs &a, float *smem, int row,
                                           int am, int bn) {
     f32x4 acc[FM > 0 ? FM : 1][4];
@@ -609,18 +610,23 @@ __device__ __forceinline__ void ring_body(const RingCtx &c, const BuildArgs &a, 
     for (int i = 0; i < (FM > 0 ? FM : 1); ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    ring_issue(c, smem, 0);
-    if (c.nst > 1) ring_issue(c, smem, 1);
+#pragma unroll
+    for (int s = 0; s < SL - 1; ++s)
+        if (s < c.nst) ring_issue<SL>(c, smem, s);
     for (int st = 0; st < c.nst; ++st) {
-        // RAW: my DMA for stage st landed (stage st+1's 4 may stay in flight);
-        // WAR: my LDS reads of stage st-1 are done.  Then the barrier.
-        if (st + 1 < c.nst) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        // RAW: my DMA for stage st landed (the later stages' 4 instructions
+        // each may stay in flight); WAR: my LDS reads of stage st-1 are done.
+        // Then the barrier.
+        const int later = min(SL - 2, c.nst - 1 - st);
+        if (later >= 3) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+        else if (later == 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else if (later == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (st + 2 < c.nst) ring_issue(c, smem, st + 2);
+        if (st + SL - 1 < c.nst) ring_issue<SL>(c, smem, st + SL - 1);
         if constexpr (FM > 0) {
-            const float *sA = smem + (st % kRingSlots) * kSlotFloats, *sB = sA + kBK * 128;
+            const float *sA = smem + (st % SL) * kSlotFloats, *sB = sA + kBK * 128;
             ring_stage<FM, FN>(sA, sB, am, bn, c.lane, acc);
         }
     }
@@ -637,9 +643,10 @@ __device__ __forceinline__ void ring_body(const RingCtx &c, const BuildArgs &a, 
 // FN = 4 B-fragments: 64-wide wave tiles, WG 128x128.  (48-wide tiles with
 // FN = 3, which avoid padding at W = 240/720, measured slower: 414 vs 372 us
 // at config 2 -- more workgroups re-read A and the B DMA/FLOP grows.)
-template <int FN, int MODE>
+template <int FN, int MODE, int SL = kRingSlots>
 __global__ __launch_bounds__(256) void build_f32_ring_kernel(BuildArgs a, int nwg_total) {
-    __shared__ __attribute__((aligned(16))) float smem[kRingSlots * kSlotFloats];
+    static_assert(SL >= 3 && SL <= 5, "ring depth");
+    __shared__ __attribute__((aligned(16))) float smem[SL * kSlotFloats];
     RingCtx c;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c.lane = threadIdx.x & 63;
@@ -661,11 +668,11 @@ __global__ __launch_bounds__(256) void build_f32_ring_kernel(BuildArgs a, int nw
     const int m0 = c.M0 + am, n0 = c.N0 + bn;
     const int rows = a.W1 - m0;
     const bool active = rows > 0 && n0 < a.W2;                         // wave-uniform
-    if (!active) ring_body<0, FN, MODE>(c, a, smem, row, am, bn);
-    else if (rows > 48) ring_body<4, FN, MODE>(c, a, smem, row, am, bn);
-    else if (rows > 32) ring_body<3, FN, MODE>(c, a, smem, row, am, bn);
-    else if (rows > 16) ring_body<2, FN, MODE>(c, a, smem, row, am, bn);
-    else ring_body<1, FN, MODE>(c, a, smem, row, am, bn);
+    if (!active) ring_body<0, FN, MODE, SL>(c, a, smem, row, am, bn);
+    else if (rows > 48) ring_body<4, FN, MODE, SL>(c, a, smem, row, am, bn);
+    else if (rows > 32) ring_body<3, FN, MODE, SL>(c, a, smem, row, am, bn);
+    else if (rows > 16) ring_body<2, FN, MODE, SL>(c, a, smem, row, am, bn);
+    else ring_body<1, FN, MODE, SL>(c, a, smem, row, am, bn);
 }
 
 template <bool VEC, int U, int MODE>
@@ -673,11 +680,11 @@ static void launch(const BuildArgs &a, unsigned nwg, hipStream_t s) {
     hipLaunchKernelGGL((build_f32_kernel<VEC, U, MODE>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
 }
 
-template <int MODE>
+template <int MODE, int SL = kRingSlots>
 static void launch_ring(const BuildArgs &a, hipStream_t s) {
     const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
     if (nwg <= 0 || nwg > 0x7FFFFFFF) return;
-    hipLaunchKernelGGL((build_f32_ring_kernel<4, MODE>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg);
+    hipLaunchKernelGGL((build_f32_ring_kernel<4, MODE, SL>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg);
 }
 
 template <bool IN_BF16, bool ALIGNED>
@@ -710,7 +717,8 @@ hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStrea
 }
 
 // RAFTCORR_BUILD_MODE (dev-only ablation, read per call): 0 = product (LDS-DMA
-// ring kernel), 2 = ring without epilogue stores; 128+flags = the direct-load
+// ring kernel, 3 slots), 2 = ring without epilogue stores, 4 / 5 = 4- / 5-slot
+// ring; 128+flags = the direct-load
 // kernel (flags 1 no operand loads, 2 no stores, 64 stagger).
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
     const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
@@ -725,6 +733,8 @@ hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
     } else {
         switch (mode) {
             case 2: rc::launch_ring<2>(a, s); break;
+            case 4: rc::launch_ring<0, 4>(a, s); break;            // 4-slot ring (dev A/B)
+            case 5: rc::launch_ring<0, 5>(a, s); break;            // 5-slot ring (dev A/B)
             case 128: rc::launch<true, 2, 0>(a, n, s); break;      // direct-load kernel
             case 130: rc::launch<true, 2, 2>(a, n, s); break;
             case 131: rc::launch<true, 2, 3>(a, n, s); break;
