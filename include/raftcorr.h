@@ -13,6 +13,8 @@
  *                   ReLU (model.py:199, :206), SURVEY.md §8f rank 1.
  *   rc_corr_lookup_chain  rc_corr_lookup for a pool-chain fp32 pyramid,
  *                   reading levels 0-1 only (the default of CorrBlock1D).
+ *   rc_corr_lookup_step  coords update + flow + lookup of one loop
+ *                   iteration in one launch.
  *   rc_corr_lookup_backward, rc_corr_build_backward  the gradient of the
  *                   path to the feature maps (autograd of model.py:267-326),
  *                   SURVEY.md §8f rank 2.
@@ -118,6 +120,22 @@ int rc_corr_lookup_chain(const void *const *pyr, const int *widths, const long *
                          int levels, int radius, const float *coords_x,
                          long coord_batch_stride, int B, int H, int W1, float *out,
                          void *stream);
+
+/* One iteration of the forward loop's corr step in one launch: the
+ * coordinate update that ends the previous iteration (coords1 + delta_flow
+ * with delta_flow[:,1] = 0, the loop tail SURVEY Appendix A D8), then
+ * flow = coords1 - coords0 (model.py:377, coords0 = coords_grid :329-332),
+ * then the lookup at the new coords1 (:376).  coords1, delta, coords1_out,
+ * flow_out: (B,2,H,W1) fp32 contiguous; delta NULL = no update (first
+ * iteration); coords1_out may alias coords1.  chain != 0 runs
+ * rc_corr_lookup_chain's kernel (its preconditions apply), else
+ * rc_corr_lookup's.  The lookup output is bit-identical to theirs at the
+ * updated coordinates; coords1_out and flow_out are bit-identical to the
+ * PyTorch ops they replace.  SURVEY.md §8f rank 4. */
+int rc_corr_lookup_step(const void *const *pyr, const int *widths, const long *pyr_ld,
+                        int pyr_dtype, int levels, int radius, int chain,
+                        const float *coords1, const float *delta, float *coords1_out,
+                        float *flow_out, int B, int H, int W1, float *out, void *stream);
 
 /* Backward of rc_corr_lookup (model.py:297-316 through grid_sample's input
  * gradient, :275): for every pixel p, level i and tap t, adds

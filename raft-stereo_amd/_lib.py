@@ -30,6 +30,8 @@ SIGNATURES = {
                                  _i, _i, _vp, _l, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "rc_corr_lookup_chain": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i,
                                   _i, _vp, _l, _i, _i, _i, _vp, _vp]),
+    "rc_corr_lookup_step": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i,
+                                 _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "rc_corr_lookup_backward": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l),
                                      _i, _i, _vp, _l, _i, _i, _i, _vp, _vp]),
     "rc_corr_build_backward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_vp),

@@ -140,6 +140,21 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True):
     return pyr
 
 
+def pool_level(src):
+    """One pyramid step (model.py:294) with rc_corr_pool: (P,1,1,W) -> (P,1,1,W//2)
+    in a row-padded buffer, the same fp32 (or bf16) ops as the build epilogue."""
+    P, W = src.shape[0], src.shape[-1]
+    out = _level_buffer(P, W // 2, src.dtype, src.device, True)
+    if P == 0:
+        return out
+    with torch.cuda.device(src.device):
+        rc = _lib.lib().rc_corr_pool(src.data_ptr(), _row_stride(src), out.data_ptr(),
+                                     _row_stride(out), P, W, _dtype_code(src.dtype),
+                                     _stream(src.device))
+    _lib.check(rc, "rc_corr_pool")
+    return out
+
+
 def _check_coords(pyramid, coords):
     _require_hip(coords, "coords")
     if coords.dim() != 4 or coords.shape[1] < 1:
@@ -210,31 +225,29 @@ def lookup(pyramid, coords, num_levels, radius):
     return out
 
 
-def chain_ok(pyramid, num_levels, radius):
-    """True when rc_corr_lookup_chain applies: an fp32 pool-chain pyramid with
-    3-4 levels, radius <= 4 and a 16-byte level-1 row stride."""
-    if num_levels not in (3, 4) or not 1 <= radius <= 4 or pyramid[0].dtype != torch.float32:
-        return False
-    if any(pyramid[i].shape[-1] != pyramid[i - 1].shape[-1] // 2 for i in range(1, num_levels)):
-        return False
-    lvl1 = pyramid[1]
-    return lvl1.stride(-1) == 1 and _row_stride(lvl1) % 4 == 0 and lvl1.data_ptr() % 16 == 0
-
-
 def lookup_chain(pyramid, coords, num_levels, radius):
     """rc_corr_lookup_chain: same result as :func:`lookup` for a pyramid whose
     levels are the avg-pool chain of level 0 (what :func:`build_pyramid`
-    writes), reading only levels 0 and 1 (include/raftcorr.h)."""
+    writes).  Only ``pyramid[0]`` and ``pyramid[1]`` are read; later entries
+    may be missing (None) -- the kernel recomputes them (include/raftcorr.h)."""
     x, cbs = _check_coords(pyramid, coords)
     B, _, H, W1 = coords.shape
     out = torch.empty((B, num_levels * (2 * radius + 1), H, W1), dtype=torch.float32,
                       device=coords.device)
     if B * H * W1 == 0:
         return out
-    keep, ptrs, widths, lds, dt = _level_args(pyramid, num_levels)
+    lv = [t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous()
+          for t in pyramid[:2]]
+    if lv[0].dtype != torch.float32 or lv[1].dtype != torch.float32:
+        raise TypeError("lookup_chain: fp32 pyramid levels required")
+    W0 = lv[0].shape[-1]
+    ptrs = [lv[0].data_ptr()] + [lv[1].data_ptr()] * (num_levels - 1)
+    lds = [_row_stride(lv[0])] + [_row_stride(lv[1])] * (num_levels - 1)
     with torch.cuda.device(coords.device):
-        rc = _lib.lib().rc_corr_lookup_chain(ptrs, widths, lds, num_levels, radius, x.data_ptr(),
-                                             cbs, B, H, W1, out.data_ptr(), _stream(coords.device))
+        rc = _lib.lib().rc_corr_lookup_chain(
+            _lib.ptr_array(ptrs), _lib.int_array([W0 >> i for i in range(num_levels)]),
+            _lib.long_array(lds), num_levels, radius, x.data_ptr(), cbs, B, H, W1,
+            out.data_ptr(), _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup_chain")
     return out
 
@@ -351,7 +364,8 @@ class _LookupFn(torch.autograd.Function):
 class CorrBlock1D:
     """model.py:283-326, on the gfx950 kernels (see module docstring)."""
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
+                 lazy_levels=None):
         self.num_levels = num_levels
         self.radius = radius
         if pyramid_dtype is None:
@@ -359,27 +373,101 @@ class CorrBlock1D:
             pyramid_dtype = torch.bfloat16 if low else torch.float32
         self.pyramid_dtype = pyramid_dtype
         grad = torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad)
+        B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+        if num_levels < 1 or (W2 >> num_levels) < 1:
+            raise RuntimeError(
+                f"CorrBlock1D: W2={W2} is too narrow for {num_levels} pooling steps: "
+                "avg_pool2d output size is too small (model.py:294)")
+        # fp32 pyramids with 3-4 levels use the chain lookup, which reads levels
+        # 0 and 1 only and recomputes levels 2.. from level 1 bit for bit
+        # (§3.2c of DESIGN.md).  Levels >= 2 are then built only when
+        # ``corr_pyramid`` is read (``lazy_levels``, default on in that case):
+        # same values, same shapes, pooled by the same fp32 ops.
+        self._chain = (pyramid_dtype == torch.float32 and num_levels in (3, 4)
+                       and 1 <= radius <= 4)
+        lazy = self._chain if lazy_levels is None else (bool(lazy_levels) and self._chain)
         with torch.no_grad():
-            self.corr_pyramid = build_pyramid(fmap1, fmap2, num_levels + 1, pyramid_dtype)
-        # levels 0..L-1 are the pool chain of level 0 (the epilogue pools the
-        # stored values): the lookup reads levels 0 and 1 only
-        self._chain = chain_ok(self.corr_pyramid, num_levels, radius)
+            nbuf = 2 if lazy else num_levels + 1
+            self._levels = build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype)
+            self._levels += [None] * (num_levels + 1 - nbuf)
         self._state = self._token = None
         if grad:
-            B, _, H, W1 = fmap1.shape
-            self._state = _GradState(B * H * W1, [t.shape[-1] for t in self.corr_pyramid[:num_levels]],
+            self._state = _GradState(B * H * W1, [W2 >> i for i in range(num_levels)],
                                      fmap1.device, num_levels, radius)
             self._token = _BuildFn.apply(fmap1, fmap2, self._state)
 
+    @property
+    def corr_pyramid(self):
+        """num_levels+1 tensors (B*H*W1, 1, 1, W2 >> l) as model.py:287-295;
+        lazily pooled levels are built on first access."""
+        if any(t is None for t in self._levels):
+            with torch.no_grad():
+                for l in range(1, len(self._levels)):
+                    if self._levels[l] is None:
+                        self._levels[l] = pool_level(self._levels[l - 1])
+        return self._levels
+
+    @corr_pyramid.setter
+    def corr_pyramid(self, levels):
+        # a replaced pyramid need not be a pool chain: use the per-level lookup
+        self._levels = list(levels)
+        self._chain = False
+
     def _lookup(self, coords):
         if self._chain:
-            return lookup_chain(self.corr_pyramid, coords, self.num_levels, self.radius)
+            return lookup_chain(self._levels, coords, self.num_levels, self.radius)
         return lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
 
     def __call__(self, coords):
         if self._token is not None and torch.is_grad_enabled():
             return _LookupFn.apply(self._token, coords.detach(), self._state, self._lookup)
         return self._lookup(coords)
+
+    def lookup_step(self, coords1, delta=None, out=None):
+        """One iteration's corr step in ONE launch:
+        ``coords1 <- coords1 + delta`` with delta's y ignored (the loop tail
+        zeroes it), ``flow = coords1 - coords_grid``
+        (model.py:377) and the lookup at the new coords1 (:376).  Returns
+        ``(corr, coords1_new, flow)``, each bit-identical to the unfused ops.
+        ``delta=None`` skips the update (first iteration); ``out=coords1``
+        updates in place.  Inference only."""
+        if self._token is not None and torch.is_grad_enabled():
+            raise RuntimeError("CorrBlock1D.lookup_step is inference-only")
+        _check_coords(self._levels, coords1)
+        B, C2, H, W1 = coords1.shape
+        if C2 != 2:
+            raise RuntimeError("lookup_step: coords1 must be (B, 2, H, W1)")
+        c1 = coords1.detach().contiguous()
+        d = None
+        if delta is not None:
+            d = delta.detach().float().contiguous()
+            if d.shape != c1.shape:
+                raise RuntimeError(f"lookup_step: delta {tuple(d.shape)} != coords {tuple(c1.shape)}")
+        new = torch.empty_like(c1) if out is None else out
+        if new.shape != c1.shape or not new.is_contiguous() or new.dtype != torch.float32:
+            raise RuntimeError("lookup_step: out must be a contiguous fp32 (B, 2, H, W1) tensor")
+        flow = torch.empty_like(c1)
+        L, r = self.num_levels, self.radius
+        corr = torch.empty((B, L * (2 * r + 1), H, W1), dtype=torch.float32, device=c1.device)
+        if B * H * W1 == 0:
+            return corr, new, flow
+        if self._chain:
+            lv = self._levels[:2]
+            W0 = lv[0].shape[-1]
+            ptrs = _lib.ptr_array([lv[0].data_ptr()] + [lv[1].data_ptr()] * (L - 1))
+            widths = _lib.int_array([W0 >> i for i in range(L)])
+            lds = _lib.long_array([_row_stride(lv[0])] + [_row_stride(lv[1])] * (L - 1))
+            dt = _lib.RC_F32
+            keep = lv
+        else:
+            keep, ptrs, widths, lds, dt = _level_args(self.corr_pyramid, L)
+        with torch.cuda.device(c1.device):
+            rc = _lib.lib().rc_corr_lookup_step(
+                ptrs, widths, lds, dt, L, r, int(self._chain), c1.data_ptr(),
+                d.data_ptr() if d is not None else None, new.data_ptr(), flow.data_ptr(),
+                B, H, W1, corr.data_ptr(), _stream(c1.device))
+        _lib.check(rc, "rc_corr_lookup_step")
+        return corr, new, flow
 
     def lookup_convc1(self, coords, weight, bias=None, relu=True):
         """``relu(convc1(self(coords)))`` in one launch:

@@ -205,6 +205,42 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
                   "rc_corr_lookup_chain: launch");
 }
 
+extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, const long *pyr_ld,
+                                   int pyr_dtype, int levels, int radius, int chain,
+                                   const float *coords1, const float *delta, float *coords1_out,
+                                   float *flow_out, int B, int H, int W1, float *out,
+                                   void *stream) {
+    g_err[0] = 0;
+    rc::LookupArgs a;
+    bool empty;
+    int rc = prep_lookup("rc_corr_lookup_step", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
+                         coords1, 2L * H * W1, B, H, W1, out, a, &empty);
+    if (rc || empty) return rc;
+    if (!coords1_out || !flow_out)
+        return fail(RC_EINVAL, "rc_corr_lookup_step: null coords1_out / flow_out");
+    if (chain) {
+        if (pyr_dtype != RC_F32 || levels < 3 || levels > 4 || radius > 4)
+            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: chain needs fp32, levels 3..4, "
+                        "radius 1..4");
+        for (int i = 1; i < levels; ++i)
+            if (widths[i] != widths[i - 1] / 2)
+                return fail(RC_EINVAL, "rc_corr_lookup_step: width %d of level %d is not "
+                            "floor(%d/2)", widths[i], i, widths[i - 1]);
+        if (a.ld[1] % 4 != 0)
+            return fail(RC_EINVAL, "rc_corr_lookup_step: level-1 row stride not a multiple of 4");
+    }
+    a.out = out;
+    a.step = 1;
+    a.W1 = W1;
+    a.delta = delta;
+    a.coords_out = coords1_out;
+    a.flow_out = flow_out;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    return hip_rc(chain ? rc_launch_lookup_chain(a, radius, s)
+                        : rc_launch_lookup(a, radius, pyr_dtype == RC_BF16, s),
+                  "rc_corr_lookup_step: launch");
+}
+
 extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
                                        const long *grad_ld, int levels, int radius,
                                        const float *coords_x, long coord_batch_stride, int B,

@@ -64,6 +64,14 @@ struct LookupArgs {
     long long P;              // B*H*W1
     int HW;                   // H*W1
     int levels;
+    // rc_corr_lookup_step only (step != 0): coords is the whole (B,2,H,W1)
+    // coords1; x = coords1.x + delta.x (delta may be null), and the advanced
+    // coords and flow = coords - coords_grid are written before the lookup
+    int step;
+    int W1;
+    const float *delta;
+    float *coords_out;
+    float *flow_out;
 };
 
 // Backward of the lookup: level gradients (fp32, row stride ld[i] % 4 == 0).

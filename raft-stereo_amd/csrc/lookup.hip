@@ -34,6 +34,32 @@
 
 namespace rc {
 
+// x coordinate of pixel (bimg, rem).  For rc_corr_lookup_step the pixel's
+// coordinates are first advanced by the previous iteration's update (the
+// forward loop's tail, SURVEY Appendix A D8: coords1 + delta_flow with the
+// y component zeroed) and the new coords and flow = coords1 - coords0
+// (model.py:377, coords0 = coords_grid, :329-332) are written -- the
+// loop's per-iteration elementwise ops, fused into the lookup launch.
+__device__ __forceinline__ float pixel_x(const LookupArgs &a, long long bimg, long long rem,
+                                         bool active) {
+    if (!a.step) return a.coords[bimg * a.cbs + rem];
+    const long long o = bimg * 2LL * a.HW + rem;   // (B,2,H,W1) contiguous
+    float x = a.coords[o];
+    float y = a.coords[o + a.HW];
+    if (a.delta) {
+        x = x + a.delta[o];
+        y = y + 0.0f;                               // delta_flow[:,1] = 0
+    }
+    if (active) {
+        const int h = (int)(rem / a.W1), w = (int)(rem - (long long)h * a.W1);
+        a.coords_out[o] = x;
+        a.coords_out[o + a.HW] = y;
+        a.flow_out[o] = x - (float)w;
+        a.flow_out[o + a.HW] = y - (float)h;
+    }
+    return x;
+}
+
 template <int R, bool BF16>
 struct LevelWindow {
     static constexpr int T = 2 * R + 1;
@@ -161,7 +187,7 @@ void lookup_kernel(LookupArgs a) {
     const bool active = p < a.P;
     const long long pp = active ? p : a.P - 1;
     const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
-    const float x = a.coords[bimg * a.cbs + rem];
+    const float x = pixel_x(a, bimg, rem, active);
     const int L = NL > 0 ? NL : a.levels;
     float *outp = a.out + bimg * (long long)(L * T) * a.HW + rem;
     const long long lrow = pp - pblk;
@@ -225,7 +251,7 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
     const bool active = p < a.P;
     const long long pp = active ? p : a.P - 1;
     const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
-    const float x = a.coords[bimg * a.cbs + rem];
+    const float x = pixel_x(a, bimg, rem, active);
     float *outp = a.out + bimg * (long long)(NL * T) * a.HW + rem;
     const long long lrow = pp - pblk;
 
@@ -367,7 +393,7 @@ __global__ __launch_bounds__(256) void lookup_conv_kernel(LookupArgs a, const fl
     const bool active = p < a.P;
     const long long pp = active ? p : a.P - 1;
     const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
-    const float x = a.coords[bimg * a.cbs + rem];
+    const float x = pixel_x(a, bimg, rem, active);
     const long long lrow = pp - pblk;
     float corr[CIN];
 #pragma unroll

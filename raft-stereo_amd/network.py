@@ -233,7 +233,7 @@ class BasicMultiUpdateBlock(nn.Module):
 class RAFTStereo(nn.Module):
     """model.py:335-383 with the correlation block pluggable (``corr_block``)."""
 
-    def __init__(self, args, corr_block=None, fuse_convc1=False):
+    def __init__(self, args, corr_block=None, fuse_convc1=False, fuse_step=False):
         super().__init__()
         self.args = args
         context_dims = args.hidden_dims
@@ -248,6 +248,9 @@ class RAFTStereo(nn.Module):
         self.corr_block = corr_block or CorrBlock1D
         # run convc1 + ReLU inside the lookup launch
         self.fuse_convc1 = fuse_convc1
+        # the loop's coords update and flow inside the
+        # lookup launch (CorrBlock1D.lookup_step); exclusive with fuse_convc1
+        self.fuse_step = fuse_step
 
     def initialize_flow(self, img):
         N, _, H, W = img.shape
@@ -280,16 +283,25 @@ class RAFTStereo(nn.Module):
         coords0, coords1 = self.initialize_flow(net_list[0])
         if flow_init is not None:
             coords1 = coords1 + flow_init
-        fused = self.fuse_convc1 and hasattr(corr_fn, "lookup_convc1")
+        step = self.fuse_step and hasattr(corr_fn, "lookup_step")
+        fused = self.fuse_convc1 and not step and hasattr(corr_fn, "lookup_convc1")
         enc = self.update_block.encoder
         predictions = []
-        for _ in range(iters):
+        delta = None
+        for itr in range(iters):
             coords1 = coords1.detach()
-            if fused:                                   # lookup + convc1 + ReLU, one launch
-                corr = corr_fn.lookup_convc1(coords1, enc.convc1.weight, enc.convc1.bias)
+            if step:
+                # previous iteration's coords update + flow + lookup, one launch;
+                # its flow is that iteration's prediction (coords1 - coords0)
+                corr, coords1, flow = corr_fn.lookup_step(coords1, delta)
+                if itr > 0:
+                    predictions.append(flow)
             else:
-                corr = corr_fn(coords1)                 # the hot path, every iteration
-            flow = coords1 - coords0
+                if fused:                               # lookup + convc1 + ReLU, one launch
+                    corr = corr_fn.lookup_convc1(coords1, enc.convc1.weight, enc.convc1.bias)
+                else:
+                    corr = corr_fn(coords1)             # the hot path, every iteration
+                flow = coords1 - coords0
             with self._autocast():
                 if a.n_gru_layers == 3 and a.slow_fast_gru:
                     net_list = self.update_block(net_list, inp_list, iter32=True, iter16=False,
@@ -300,7 +312,14 @@ class RAFTStereo(nn.Module):
                 net_list, up_mask, delta_flow = self.update_block(
                     net_list, inp_list, corr, flow, iter32=a.n_gru_layers == 3,
                     iter16=a.n_gru_layers >= 2, corr_is_convc1=fused)
+            if step:
+                delta = delta_flow.float()              # applied by the next launch
+                continue
             delta_flow[:, 1] = 0.0                       # D8 tail (see module docstring)
             coords1 = coords1 + delta_flow.float()
+            predictions.append(coords1 - coords0)
+        if step and delta is not None:                   # the last iteration's update
+            delta[:, 1] = 0.0
+            coords1 = coords1 + delta
             predictions.append(coords1 - coords0)
         return predictions

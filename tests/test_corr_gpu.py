@@ -372,3 +372,61 @@ def test_lookup_convc1_vs_separate(L, r, pyr_dt, bias, relu):
             ref = torch.relu(ref)
     assert fused.shape == ref.shape
     assert norm_err(fused.cpu().numpy(), ref.cpu().numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 3, 240, 240, 4, 4), (1, 32, 2, 311, 311, 3, 3),
+                                   (1, 16, 2, 45, 61, 4, 2)], ids=lambda s: "x".join(map(str, s)))
+def test_lazy_levels_equal_fused_epilogue(shape):
+    """Default fp32 blocks write levels 0-1 in the build and pool levels >= 2
+    on first access to corr_pyramid; the eager build writes every level in
+    the fused epilogue.  Same values bit for bit, same lookups."""
+    B, D, H, W1, W2, L, r = shape
+    g = torch.Generator().manual_seed(1234 + sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    coords = special_coords(B, H, W1, W2, g).to(DEV)
+    with torch.no_grad():
+        lazy = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        eager = CorrBlock1D(f1, f2, num_levels=L, radius=r, lazy_levels=False)
+        assert lazy._levels[2] is None and eager._levels[2] is not None
+        a, b = lazy(coords), eager(coords)
+        assert lazy._levels[2] is None                 # the lookup did not need them
+    assert same(a.cpu().numpy(), b.cpu().numpy())
+    pl, pe = pyr_np(lazy), pyr_np(eager)
+    assert len(pl) == len(pe) == L + 1
+    for i in range(L + 1):
+        assert lazy.corr_pyramid[i].shape == eager.corr_pyramid[i].shape
+        assert same(pl[i], pe[i]), f"level {i}"
+
+
+@pytest.mark.parametrize("L,r,pyr_dt", [(4, 4, torch.float32), (3, 3, torch.float32),
+                                        (2, 4, torch.float32), (4, 4, torch.bfloat16)])
+def test_lookup_step_matches_unfused(L, r, pyr_dt):
+    """rc_corr_lookup_step == the loop's PyTorch ops
+    (coords1 + delta with delta[:,1] = 0; flow = coords1 - coords_grid) and
+    the plain lookup at the new coords, bit for bit; also in place."""
+    g = torch.Generator().manual_seed(40 + L + r)
+    B, D, H, W1, W2 = 2, 32, 5, 96, 96
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    c0 = rcorr.coords_grid(B, H, W1).to(DEV)
+    c1 = c0.clone()
+    c1[:, 0] -= (torch.rand(B, H, W1, generator=g) * 30).to(DEV)
+    delta = (torch.randn(B, 2, H, W1, generator=g) * 3).to(DEV)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=pyr_dt)
+        corr, new, flow = blk.lookup_step(c1, delta)
+        d = delta.clone()
+        d[:, 1] = 0.0
+        ref_new = c1 + d
+        assert torch.equal(new, ref_new)
+        assert torch.equal(flow, ref_new - c0)
+        assert same(corr.cpu().numpy(), blk(ref_new).cpu().numpy())
+        # first iteration (no delta) and in-place update
+        corr0, new0, flow0 = blk.lookup_step(c1)
+        assert torch.equal(new0, c1) and torch.equal(flow0, c1 - c0)
+        assert same(corr0.cpu().numpy(), blk(c1).cpu().numpy())
+        buf = c1.clone()
+        corr2, new2, _ = blk.lookup_step(buf, delta, out=buf)
+        assert new2.data_ptr() == buf.data_ptr() and torch.equal(buf, ref_new)
+        assert same(corr2.cpu().numpy(), corr.cpu().numpy())

@@ -64,3 +64,25 @@ def test_disparity_with_fused_convc1(name):
     disp = np.stack([f[:, 0].cpu().numpy() for f in flows], 0)
     mae = np.abs(disp - z["disparity"]).mean(axis=(1, 2, 3))
     assert (mae <= MAE_PX).all(), f"per-iteration MAE {mae}"
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_disparity_with_fused_step(name):
+    """The network with the coords update + flow fused into the lookup launch
+     gives the same per-iteration disparity as the unfused
+    network, bit for bit, and so stays within the north_star bar."""
+    case = CASES[name]
+    z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
+    img1, img2 = torch.from_numpy(z["image1"]).cuda(), torch.from_numpy(z["image2"]).cuda()
+    outs = []
+    for fuse in (False, True):
+        torch.manual_seed(0)
+        model = RAFTStereo(StereoArgs(**case["args"]), fuse_step=fuse).eval().cuda()
+        with torch.no_grad():
+            outs.append([f.cpu() for f in model(img1, img2, iters=int(z["iters"]))])
+    assert len(outs[0]) == len(outs[1]) == int(z["iters"])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    disp = np.stack([f[:, 0].numpy() for f in outs[1]], 0)
+    mae = np.abs(disp - z["disparity"]).mean(axis=(1, 2, 3))
+    assert (mae <= MAE_PX).all(), f"per-iteration MAE {mae}"
