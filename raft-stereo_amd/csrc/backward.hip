@@ -34,6 +34,8 @@
 //     rows), so each lane ends with 4 consecutive n of one d row: 16-byte
 //     output stores.  The workgroups of one (b,h) row are remapped onto one
 //     XCD, which then reads that row's operands from HBM once.
+#include <type_traits>
+
 #include "common.h"
 
 namespace rc {
@@ -120,6 +122,226 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(LookupBwdArgs a) {
             *reinterpret_cast<f32x4 *>(row + cs) = v;
         }
     }
+}
+
+// ------------------------------------------------ lookup bwd, pool chain
+// The build's backward folds the level gradients through avg_pool2d's
+// backward (Dl_i[k] = g_i[k] + Dl_{i+1}[k>>1] / 2), which is linear: a
+// gradient c on level-i element j reaches each of level-1 elements
+// [2^(i-1) j, 2^(i-1) (j+1)) as c / 2^(i-1).  This kernel adds levels >= 2
+// there directly, so -- like the forward chain lookup (lookup.hip) -- it
+// touches one level-0 window and one level-1 span per pixel instead of one
+// window per level, and the build backward folds two buffers.  All loads
+// (grad_out, both read-modify-write ranges) are issued before any math: one
+// memory round trip per wave.  Taps that fall outside the register windows
+// (unreachable within the round trip's error bound, or a subnormal x) are
+// applied after the chunk stores with direct read-modify-writes.
+
+// Direct read-modify-write of the taps in `mask` of level i (the chain
+// backward's rare off-window path).  Out of line: inlined, its recomputed
+// tap coordinates would be merged with the main path's and kept live.
+__device__ __attribute__((noinline)) void bwd_chain_fallback(const LookupBwdArgs &a, int i, int R,
+                                                            float x, float *row, const float *go,
+                                                            unsigned mask) {
+    const int T = 2 * R + 1, SI = i == 0 ? 1 : 1 << (i - 1);
+    const float scale = 1.0f / (float)SI;
+    const float Wm1 = (float)(a.W[i] - 1), half = Wm1 / 2.0f;
+    const float xl = x / (float)(1 << i);
+    for (int t = 0; t < T; ++t) {
+        if (!((mask >> t) & 1u)) continue;
+        const float xt = (float)(t - R) + xl;
+        const float xn = (2.0f * xt) / Wm1 - 1.0f;
+        const float xp = (xn + 1.0f) * half;
+        const float x0 = floorf(xp);
+        const float w1 = xp - x0, w0 = (x0 + 1.0f) - xp;
+        const float g = go[(long long)(i * T + t) * a.HW];
+        if (x0 >= 0.0f && x0 <= Wm1)
+            for (int c = 0; c < SI; ++c) row[SI * (long long)x0 + c] += w0 * g * scale;
+        if (x0 + 1.0f >= 0.0f && x0 + 1.0f <= Wm1)
+            for (int c = 0; c < SI; ++c) row[SI * ((long long)x0 + 1) + c] += w1 * g * scale;
+    }
+}
+
+template <int R, int NL>
+__global__ __launch_bounds__(256) void lookup_bwd_chain_kernel(LookupBwdArgs a) {
+    static_assert(NL >= 3 && NL <= 4, "chain backward: 3 or 4 levels");
+    constexpr int T = 2 * R + 1, NW = 2 * R + 4, NV0 = (NW + 6) / 4;
+    constexpr int TOP = NL - 1, S = 1 << (TOP - 1);
+    constexpr int NE1 = S * NW, SHM = (S % 4 == 0) ? 0 : 4 - S, NC1 = (NE1 + SHM + 3) / 4;
+    // the level-1 span accumulator, one private column per lane ([k][lane]:
+    // lane-consecutive addresses, conflict-free for any per-lane k)
+    __shared__ float span[NE1][256];
+    const int lane = threadIdx.x;
+    const long long p = (long long)blockIdx.x * 256 + lane;
+    if (p >= a.P) return;   // no barriers in this kernel
+    const long long bimg = p / a.HW, rem = p - bimg * a.HW;
+    const float x = a.coords[bimg * a.cbs + rem];
+    const float *go = a.grad_out + bimg * (long long)(NL * T) * a.HW + rem;
+
+    // level 0: window [e00, e00 + NW), touched span [f0, l0]
+    float *row0 = a.g[0] + p * a.ld[0];
+    const int W0 = a.W[0];
+    const float Wm10 = (float)(W0 - 1), half0 = Wm10 / 2.0f;
+    const bool inwin0 = (x > -(float)(R + 4)) && (x < (float)(W0 + R + 4));
+    const float n0 = inwin0 ? floorf(x) : 0.0f;
+    int f0 = 1, l0 = 0;
+    if (inwin0) {
+        const float pa = ((2.0f * ((float)(-R) + x)) / Wm10 - 1.0f + 1.0f) * half0;
+        const float pb = ((2.0f * ((float)R + x)) / Wm10 - 1.0f + 1.0f) * half0;
+        f0 = max((int)floorf(pa), 0);
+        l0 = min((int)floorf(pb) + 1, W0 - 1);
+    }
+    const int e00 = (int)n0 - R - 1, ea0 = e00 & ~3, sh0 = e00 - ea0;
+    f32x4 v0[NV0];
+#pragma unroll
+    for (int k = 0; k < NV0; ++k) {
+        const int cs = ea0 + 4 * k;
+        v0[k] = (f0 <= l0 && cs <= l0 && cs + 3 >= f0) ? *reinterpret_cast<const f32x4 *>(row0 + cs)
+                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // levels 1..TOP: one level-1 span [e1, e1 + NE1), e1 = S (n_top - R - 1);
+    // union of the touched elements [lo, hi] (level-1 coordinates)
+    float *row1 = a.g[1] + p * a.ld[1];
+    const float xtop = x / (float)(1 << TOP);
+    const bool inwin = (xtop > -(float)(R + 4)) && (xtop < (float)(a.W[TOP] + R + 4));
+    const float ntop = inwin ? floorf(xtop) : 0.0f;
+    const int e1 = S * ((int)ntop - R - 1), ea1 = e1 & ~3, sh1 = e1 - ea1;
+    int lo = 0x7FFFFFFF, hi = -1;
+    if (inwin) {
+#pragma unroll
+        for (int i = 1; i <= TOP; ++i) {
+            const float Wm1 = (float)(a.W[i] - 1), half = Wm1 / 2.0f;
+            const float xl = x / (float)(1 << i);
+            const float pa = ((2.0f * ((float)(-R) + xl)) / Wm1 - 1.0f + 1.0f) * half;
+            const float pb = ((2.0f * ((float)R + xl)) / Wm1 - 1.0f + 1.0f) * half;
+            const int f = max((int)floorf(pa), 0), l = min((int)floorf(pb) + 1, a.W[i] - 1);
+            if (f <= l) {
+                lo = min(lo, f << (i - 1));
+                hi = max(hi, ((l + 1) << (i - 1)) - 1);
+            }
+        }
+    }
+    f32x4 v1[NC1];
+#pragma unroll
+    for (int k = 0; k < NC1; ++k) {
+        const int cs = ea1 + 4 * k;
+        v1[k] = (cs <= hi && cs + 3 >= lo) ? *reinterpret_cast<const f32x4 *>(row1 + cs)
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < NE1; ++k) span[k][lane] = 0.0f;
+
+    unsigned fallback[NL];   // per level: taps left for the direct path (bit t)
+    {   // level 0 -> register window -> its chunks
+        float acc[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) acc[j] = 0.0f;
+        fallback[0] = 0u;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + x;
+            const float xn = (2.0f * xt) / Wm10 - 1.0f;       // model.py:271
+            const float xp = (xn + 1.0f) * half0;              // :275
+            const float x0 = floorf(xp);
+            const float w1 = xp - x0, w0 = (x0 + 1.0f) - xp;
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm10);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm10);
+            if (!(ok0 || ok1)) continue;
+            const float nt = n0 + (float)(t - R);
+            if (!inwin0 || x0 < nt - 1.0f || x0 > nt + 1.0f) {
+                fallback[0] |= 1u << t;
+                continue;
+            }
+            const float g = go[(long long)t * a.HW];
+            const float c0 = w0 * g, c1 = w1 * g;
+            const int j0 = t + (x0 < nt ? 0 : (x0 > nt ? 2 : 1));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = t + q;
+                if (j < NW) {
+                    float add = acc[j];
+                    if (ok0 && j0 == j) add += c0;
+                    if (ok1 && j0 + 1 == j) add += c1;
+                    acc[j] = add;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NV0; ++k)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float add = 0.0f;   // acc[4k + c - sh0]
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int j = 4 * k + c - s;
+                    if (j >= 0 && j < NW) add = (sh0 == s) ? acc[j] : add;
+                }
+                v0[k][c] += add;
+            }
+    }
+    // levels 1..TOP -> the span: a gradient c on level-i element e lands on
+    // level-1 elements [SI e, SI e + SI) as c / SI (SI = 2^(i-1))
+#pragma unroll
+    for (int i = 1; i <= TOP; ++i) {
+        const int SI = 1 << (i - 1);
+        const float scale = 1.0f / (float)SI;
+        const float Wm1 = (float)(a.W[i] - 1), half = Wm1 / 2.0f;
+        const float xl = x / (float)(1 << i);
+        fallback[i] = 0u;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + xl;
+            const float xn = (2.0f * xt) / Wm1 - 1.0f;
+            const float xp = (xn + 1.0f) * half;
+            const float x0 = floorf(xp);
+            const float w1 = xp - x0, w0 = (x0 + 1.0f) - xp;
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            if (!(ok0 || ok1)) continue;
+            // level-1 offset of element x0 inside the span (x0 in [-1, W_i])
+            const int off = inwin ? SI * (int)x0 - e1 : -1;
+            if (off < 0 || off + 2 * SI > NE1) {
+                fallback[i] |= 1u << t;
+                continue;
+            }
+            const float g = go[(long long)(i * T + t) * a.HW];
+            const float c0 = w0 * g * scale, c1 = w1 * g * scale;
+            for (int c = 0; c < SI; ++c) {
+                if (ok0) span[off + c][lane] += c0;
+                if (ok1) span[off + SI + c][lane] += c1;
+            }
+        }
+    }
+    // span element k sits at register element k + sh1 of the loaded chunks
+#pragma unroll
+    for (int k = 0; k < NE1; ++k) {
+        const float add = span[k][lane];
+        if constexpr (SHM == 0) {
+            v1[k >> 2][k & 3] += add;
+        } else {
+#pragma unroll
+            for (int s = 0; s <= SHM; ++s)
+                if (k + s < 4 * NC1) v1[(k + s) >> 2][(k + s) & 3] += (sh1 == s) ? add : 0.0f;
+        }
+    }
+
+    // write back the chunks that were read (each inside the lane's own row)
+#pragma unroll
+    for (int k = 0; k < NV0; ++k) {
+        const int cs = ea0 + 4 * k;
+        if (f0 <= l0 && cs <= l0 && cs + 3 >= f0) *reinterpret_cast<f32x4 *>(row0 + cs) = v0[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NC1; ++k) {
+        const int cs = ea1 + 4 * k;
+        if (cs <= hi && cs + 3 >= lo) *reinterpret_cast<f32x4 *>(row1 + cs) = v1[k];
+    }
+
+    // off-window taps: direct read-modify-writes (after the chunk stores)
+#pragma unroll
+    for (int i = 0; i < NL; ++i)
+        if (__builtin_expect(fallback[i] != 0u, 0))
+            bwd_chain_fallback(a, i, R, x, i == 0 ? row0 : row1, go, fallback[i]);
 }
 
 // ---------------------------------------------------------------- volume bwd
@@ -323,6 +545,24 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
         case 8: hipLaunchKernelGGL(rc::lookup_bwd_kernel<8>, dim3(nblk), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t rc_launch_lookup_bwd_chain(const rc::LookupBwdArgs &a, int radius, hipStream_t s) {
+    if (a.P <= 0) return hipSuccess;
+    const unsigned nblk = (unsigned)((a.P + 255) / 256);
+#define RC_BWD_CHAIN(R)                                                                          \
+    if (a.levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_chain_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((rc::lookup_bwd_chain_kernel<R, 3>), dim3(nblk), dim3(256), 0, s, a);
+    if (a.levels != 3 && a.levels != 4) return hipErrorInvalidValue;
+    switch (radius) {
+        case 1: RC_BWD_CHAIN(1) break;
+        case 2: RC_BWD_CHAIN(2) break;
+        case 3: RC_BWD_CHAIN(3) break;
+        case 4: RC_BWD_CHAIN(4) break;
+        default: return hipErrorInvalidValue;
+    }
+#undef RC_BWD_CHAIN
     return hipGetLastError();
 }
 
