@@ -169,16 +169,26 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
     widths = [W2 >> i for i in range(L)]
     g = torch.Generator().manual_seed(99)
     gouts = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(2)]
-    grads = rcorr.grad_buffers(P, widths, dev)
+    # what CorrBlock1D's autograd runs: the chain backward (two buffers) for
+    # 3-4 levels and r <= 4, else one buffer per level
+    chain = L in (3, 4) and r <= 4
+    grads = rcorr.grad_buffers(P, widths[:2] if chain else widths, dev)
+
+    def lbwd(c, go):
+        if chain:
+            rcorr.lookup_backward_chain(grads, widths, c, go, L, r)
+        else:
+            rcorr.lookup_backward(grads, c, go, L, r)
+
     for _ in range(2):   # warm-up
-        rcorr.lookup_backward(grads, coords[0], gouts[0], L, r)
+        lbwd(coords[0], gouts[0])
         rcorr.build_backward(f1, f2, grads)
     lb, vb = [], []
     for _ in range(reps):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 2)]
         ev[0].record()
         for it in range(iters):
-            rcorr.lookup_backward(grads, coords[it], gouts[it % 2], L, r)
+            lbwd(coords[it], gouts[it % 2])
             ev[it + 1].record()
         rcorr.build_backward(f1, f2, grads)
         ev[iters + 1].record()
@@ -215,7 +225,8 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": lbytes / (lb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                     "algorithmic_bytes": lbytes,
-                                    "kernel": f"rc::lookup_bwd_kernel<{r}>"},
+                                    "kernel": (f"rc::lookup_bwd_chain_kernel<{r},{L}>" if chain
+                                               else f"rc::lookup_bwd_kernel<{r}>")},
             "note": "step = CorrBlock1D build + lookups + autograd backward to both fmaps "
                     "(random output gradients); kernel times are medians of event-timed launches"}
 
