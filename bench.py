@@ -169,16 +169,10 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
     widths = [W2 >> i for i in range(L)]
     g = torch.Generator().manual_seed(99)
     gouts = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(2)]
-    # what CorrBlock1D's autograd runs: the chain backward (two buffers) for
-    # 3-4 levels and r <= 4, else one buffer per level
-    chain = L in (3, 4) and r <= 4
-    grads = rcorr.grad_buffers(P, widths[:2] if chain else widths, dev)
+    grads = rcorr.grad_buffers(P, widths, dev)
 
     def lbwd(c, go):
-        if chain:
-            rcorr.lookup_backward_chain(grads, widths, c, go, L, r)
-        else:
-            rcorr.lookup_backward(grads, c, go, L, r)
+        rcorr.lookup_backward(grads, c, go, L, r)
 
     for _ in range(2):   # warm-up
         lbwd(coords[0], gouts[0])
@@ -220,13 +214,12 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
             "roofline_volume_bwd": {"bound": "mfma", "achieved": vflops / (vb_ms * 1e-3) / 1e12,
                                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                     "frac": vflops / (vb_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                                    "kernel": "rc::volume_bwd_kernel<true>"},
+                                    "kernel": f"rc::volume_bwd_kernel<true,{L}>"},
             "roofline_lookup_bwd": {"bound": "hbm", "achieved": lbytes / (lb_ms * 1e-3) / 1e9,
                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": lbytes / (lb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                     "algorithmic_bytes": lbytes,
-                                    "kernel": (f"rc::lookup_bwd_chain_kernel<{r},{L}>" if chain
-                                               else f"rc::lookup_bwd_kernel<{r}>")},
+                                    "kernel": f"rc::lookup_bwd_kernel<{r}>"},
             "note": "step = CorrBlock1D build + lookups + autograd backward to both fmaps "
                     "(random output gradients); kernel times are medians of event-timed launches"}
 

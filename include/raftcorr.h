@@ -152,20 +152,6 @@ int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long
                             long coord_batch_stride, int B, int H, int W1,
                             const float *grad_out, void *stream);
 
-/* Backward of the chain lookup with two gradient buffers: grad0 gets level
- * 0's gradient and grad1 gets level 1's plus every level i >= 2 already
- * folded through avg_pool2d's backward (a gradient c on level-i element j
- * adds c / 2^(i-1) to each of level-1 elements [2^(i-1) j, 2^(i-1) (j+1))).
- * rc_corr_build_backward with levels = 2 over {grad0, grad1} then gives the
- * same fmap gradients as the per-level buffers (up to summation order), and
- * each pixel touches one level-0 window and one level-1 span.  Accumulates
- * like rc_corr_lookup_backward.  levels 3..4, radius 1..4, widths a pool
- * chain (widths[i] == widths[i-1] / 2), ld0 and ld1 multiples of 4. */
-int rc_corr_lookup_backward_chain(void *grad0, long ld0, void *grad1, long ld1,
-                                  const int *widths, int levels, int radius,
-                                  const float *coords_x, long coord_batch_stride,
-                                  int B, int H, int W1, const float *grad_out, void *stream);
-
 /* Backward of rc_corr_build (model.py:284-295 pooling, :318-326 volume):
  *   Dl_{L-1} = grad_pyr[L-1], Dl_i[k] = grad_pyr[i][k] + Dl_{i+1}[k/2] / 2
  *   (avg_pool2d's backward, floor widths), G = Dl_0 / sqrtf(D), and

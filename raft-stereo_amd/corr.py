@@ -285,26 +285,6 @@ def lookup_backward(grads, coords, grad_out, num_levels, radius):
     _lib.check(rc, "rc_corr_lookup_backward")
 
 
-def lookup_backward_chain(grads, widths, coords, grad_out, num_levels, radius):
-    """rc_corr_lookup_backward_chain: like :func:`lookup_backward` into TWO
-    buffers (levels 0 and 1, from :func:`grad_buffers` with widths[:2]);
-    levels >= 2 are folded into the level-1 buffer on the fly."""
-    x, cbs = _check_coords(grads, coords)
-    B, _, H, W1 = coords.shape
-    if B * H * W1 == 0:
-        return
-    go = grad_out.detach().float().contiguous()
-    if go.shape != (B, num_levels * (2 * radius + 1), H, W1):
-        raise RuntimeError(f"lookup_backward_chain: grad_out shape {tuple(go.shape)}")
-    g0, g1 = grads
-    with torch.cuda.device(coords.device):
-        rc = _lib.lib().rc_corr_lookup_backward_chain(
-            g0.data_ptr(), g0.stride(0), g1.data_ptr(), g1.stride(0),
-            _lib.int_array(list(widths[:num_levels])), num_levels, radius, x.data_ptr(), cbs,
-            B, H, W1, go.data_ptr(), _stream(coords.device))
-    _lib.check(rc, "rc_corr_lookup_backward_chain")
-
-
 def build_backward(fmap1, fmap2, grads):
     """rc_corr_build_backward: level gradients -> (d fmap1, d fmap2), fp32.
     The pooling backward (model.py:294), the 1/sqrt(D) (:326) and the two
@@ -334,19 +314,12 @@ class _GradState:
     def __init__(self, P, widths, device, num_levels, radius):
         self.P, self.widths, self.device = P, widths, device
         self.num_levels, self.radius = num_levels, radius
-        # 3-4 levels, r <= 4: two buffers, levels >= 2 folded into level 1
-        self.chain = num_levels in (3, 4) and 1 <= radius <= 4
         self.grads = None
 
     def accumulate(self, coords, grad_out):
         if self.grads is None:
-            n = 2 if self.chain else len(self.widths)
-            self.grads = grad_buffers(self.P, self.widths[:n], self.device)
-        if self.chain:
-            lookup_backward_chain(self.grads, self.widths, coords, grad_out, self.num_levels,
-                                  self.radius)
-        else:
-            lookup_backward(self.grads, coords, grad_out, self.num_levels, self.radius)
+            self.grads = grad_buffers(self.P, self.widths, self.device)
+        lookup_backward(self.grads, coords, grad_out, self.num_levels, self.radius)
 
     def take(self):
         g, self.grads = self.grads, None

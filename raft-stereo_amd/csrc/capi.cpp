@@ -270,48 +270,6 @@ extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
                   "rc_corr_lookup_backward: launch");
 }
 
-extern "C" int rc_corr_lookup_backward_chain(void *grad0, long ld0, void *grad1, long ld1,
-                                             const int *widths, int levels, int radius,
-                                             const float *coords_x, long coord_batch_stride,
-                                             int B, int H, int W1, const float *grad_out,
-                                             void *stream) {
-    g_err[0] = 0;
-    if (levels < 3 || levels > 4 || radius < 1 || radius > 4)
-        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_backward_chain: levels 3..4, radius 1..4 only");
-    if (!widths) return fail(RC_EINVAL, "rc_corr_lookup_backward_chain: null widths");
-    for (int i = 1; i < levels; ++i)
-        if (widths[i] != widths[i - 1] / 2)
-            return fail(RC_EINVAL, "rc_corr_lookup_backward_chain: width %d of level %d is not "
-                        "floor(%d/2)", widths[i], i, widths[i - 1]);
-    const void *pyr[RC_MAX_LEVELS];
-    long ld[RC_MAX_LEVELS];
-    for (int i = 0; i < levels; ++i) {
-        pyr[i] = i == 0 ? grad0 : grad1;
-        ld[i] = i == 0 ? ld0 : ld1;
-    }
-    rc::LookupArgs la;
-    bool empty;
-    int rc = prep_lookup("rc_corr_lookup_backward_chain", pyr, widths, ld, RC_F32, levels, radius,
-                         coords_x, coord_batch_stride, B, H, W1, grad_out, la, &empty);
-    if (rc || empty) return rc;
-    if (ld0 % 4 != 0 || ld1 % 4 != 0)
-        return fail(RC_EINVAL, "rc_corr_lookup_backward_chain: row strides must be multiples of 4");
-    rc::LookupBwdArgs a{};
-    for (int i = 0; i < levels; ++i) {
-        a.g[i] = static_cast<float *>(i == 0 ? grad0 : grad1);
-        a.W[i] = widths[i];
-        a.ld[i] = ld[i];
-    }
-    a.coords = coords_x;
-    a.cbs = coord_batch_stride;
-    a.grad_out = grad_out;
-    a.P = la.P;
-    a.HW = la.HW;
-    a.levels = levels;
-    return hip_rc(rc_launch_lookup_bwd_chain(a, radius, reinterpret_cast<hipStream_t>(stream)),
-                  "rc_corr_lookup_backward_chain: launch");
-}
-
 extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int fmap_dtype, int B,
                                       int D, int H, int W1, int W2, const void *const *grad_pyr,
                                       const long *grad_ld, int levels, float *grad_fmap1,

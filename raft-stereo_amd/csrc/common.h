@@ -113,5 +113,4 @@ hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf
                                  const float *b, int cout, int relu, float *out, hipStream_t s);
 hipError_t rc_launch_lookup_chain(const rc::LookupArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
-hipError_t rc_launch_lookup_bwd_chain(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s);

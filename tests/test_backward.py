@@ -180,36 +180,3 @@ def test_backward_bf16_fmaps_and_unused_lookup():
     with torch.no_grad():
         out = CorrBlock1D(h1, h1, num_levels=2, radius=2)(c)
     assert out.grad_fn is None
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(2, 3, 240, 240, 4, 4, 3), (1, 2, 311, 311, 4, 3, 2),
-                                   (1, 2, 60, 61, 3, 4, 2), (2, 2, 33, 130, 3, 2, 3),
-                                   (1, 2, 20, 16, 4, 1, 2)],
-                         ids=lambda s: "x".join(map(str, s)))
-def test_lookup_backward_chain_vs_oracle(shape):
-    """rc_corr_lookup_backward_chain: level 0 as the per-level backward;
-    level 1 = levels 1..L-1 folded through the pooling backward (oracle
-    per-level gradients folded with coracle.fold_grads).  Coordinates include
-    far-OOB, negative, integer and subnormal x."""
-    from raft_stereo_amd import corr as rcorr
-    B, H, W1, W2, L, r, calls = shape
-    g = torch.Generator().manual_seed(500 + sum(shape))
-    widths = [W2 >> i for i in range(L)]
-    P = B * H * W1
-    grads = rcorr.grad_buffers(P, widths[:2], torch.device(DEV))
-    gr = None
-    for k in range(calls):
-        x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 64
-        x[..., ::6] = torch.randint(-30, W2 + 30, x[..., ::6].shape, generator=g).float()
-        flat = x.reshape(-1)
-        flat[:6] = torch.tensor([1e30, -1e30, 0.0, -1e-45, 3e-39, float(W2) + 3.5])
-        c = torch.cat([x, torch.zeros_like(x)], 1)
-        go = torch.randn(B, L * (2 * r + 1), H, W1, generator=g)
-        rcorr.lookup_backward_chain(grads, widths, c.to(DEV), go.to(DEV), L, r)
-        gr = coracle.corr_lookup_backward(widths, c.numpy(), go.numpy(), L, r, gr)
-    g0 = grads[0].cpu().numpy()
-    g1 = grads[1].cpu().numpy()
-    assert norm_err(g0, gr[0]) <= 1e-6
-    folded1 = coracle.fold_grads(gr[1:])[0]
-    assert norm_err(g1, folded1) <= 1e-6 and rel_l2(g1, folded1) <= 1e-6

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--staggers", default="", help="RAFTCORR_STAGGER values to try with mode 64")
     ap.add_argument("--chain", action="store_true",
                     help="time rc_corr_lookup_chain vs the per-level rc_corr_lookup")
+    ap.add_argument("--bwd", action="store_true",
+                    help="time the backward kernels")
     ap.add_argument("--convc1", action="store_true",
                     help="also time lookup+convc1+relu fused vs separate (MIOpen 1x1 conv)")
     a = ap.parse_args()
@@ -90,6 +92,18 @@ def main():
                 res.setdefault("lookup_chain", []).extend(t)
                 t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, c, L, r), 8)
                 res.setdefault("lookup_perlevel", []).extend(t)
+        if a.bwd:
+            P = B * H * W1
+            widths = [W2 >> i for i in range(L)]
+            g = torch.Generator().manual_seed(9)
+            go = torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev)
+            gper = rcorr.grad_buffers(P, widths, dev)
+            for rnd in range(a.rounds):
+                c = coords[rnd % iters]
+                t = time_launches(lambda: rcorr.lookup_backward(gper, c, go, L, r), 8)
+                res.setdefault("lookup_bwd", []).extend(t)
+                t = time_launches(lambda: rcorr.build_backward(f1, f2, gper), 2)
+                res.setdefault("volume_bwd", []).extend(t)
         if a.convc1:
             conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1).to(dev)
             for rnd in range(a.rounds):
