@@ -224,6 +224,35 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
                     "(random output gradients); kernel times are medians of event-timed launches"}
 
 
+def upsample_timing(cfg, device, reps=20):
+    """Convex upsampler on the config's low-resolution
+    x-flow and a synthetic (B, 9*16, H, W) mask: event-timed launches and the
+    HBM roofline (mask + flow read, full-resolution flow written)."""
+    from raft_stereo_amd.upsample import convex_upsample
+    B, D, H, W1, W2, L, r, iters, _ = cfg
+    f = 4
+    g = torch.Generator().manual_seed(5)
+    flow = (torch.randn(B, 1, H, W1, generator=g) * 8).to(device)
+    mask = torch.randn(B, 9 * f * f, H, W1, generator=g).to(device)
+    for _ in range(3):
+        convex_upsample(flow, mask, f)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record()
+    for k in range(reps):
+        convex_upsample(flow, mask, f)
+        ev[k + 1].record()
+    torch.cuda.synchronize()
+    ts = sorted(ev[k].elapsed_time(ev[k + 1]) for k in range(reps))
+    ms = ts[len(ts) // 2]
+    nbytes = 4 * B * H * W1 * (9 * f * f + 1 + f * f)
+    return {"us": ms * 1e3, "bytes": nbytes,
+            "roofline": {"bound": "hbm", "achieved": nbytes / (ms * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "kernel": "rc::convex_upsample_kernel<4>"},
+            "shape": {"flow": [B, 1, H, W1], "mask": [B, 9 * f * f, H, W1], "factor": f}}
+
+
 def load_traffic(path):
     try:
         with open(path) as fh:
@@ -430,6 +459,7 @@ def main():
     }
     if not args.no_backward and args.config == "sceneflow":
         result["backward"] = backward_timing(cfg, f1, f2, coords)
+        result["upsample"] = upsample_timing(cfg, device)
     if args.e2e_steps > 0 and args.config == "sceneflow":
         result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1)
         result["e2e"]["pairs_per_s_all_ranks"] = result["e2e"]["pairs_per_s"] * world

@@ -15,6 +15,8 @@
  *                   reading levels 0-1 only (the default of CorrBlock1D).
  *   rc_corr_lookup_step  coords update + flow + lookup of one loop
  *                   iteration in one launch.
+ *   rc_convex_upsample  the convex upsampler for the mask the update block
+ *                   produces.
  *   rc_corr_lookup_backward, rc_corr_build_backward  the gradient of the
  *                   path to the feature maps (autograd of model.py:267-326),
  *                   SURVEY.md §8f rank 2.
@@ -164,6 +166,17 @@ int rc_corr_build_backward(const void *fmap1, const void *fmap2, int fmap_dtype,
                            int B, int D, int H, int W1, int W2,
                            const void *const *grad_pyr, const long *grad_ld, int levels,
                            float *grad_fmap1, float *grad_fmap2, void *stream);
+
+/* Convex upsampling with the update block's mask
+ * (model.py:238-241, 0.25-scaled at :264; f = 2^n_downsample, :236):
+ *   out[n][c][f h + i][f w + j] = sum_k softmax_k(mask[n][k f^2 + i f + j][h][w])
+ *                                 * f * flow[n][c][h + dy_k][w + dx_k]
+ *   k = 3 (dy+1) + (dx+1), zeros outside the image (RAFT-Stereo's upsampler,
+ *   F.unfold + softmax; the reference builds the mask but never applies it).
+ *   flow (N,C,H,W), mask (N,9f^2,H,W), out (N,C,fH,fW): fp32 contiguous.
+ *   factor 1, 2, 4 or 8. */
+int rc_convex_upsample(const float *flow, const float *mask, int N, int C, int H, int W,
+                       int factor, float *out, void *stream);
 
 #ifdef __cplusplus
 }

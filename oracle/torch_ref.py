@@ -55,3 +55,16 @@ class TorchCorrBlock1D:
             grid = torch.cat([x0, torch.zeros_like(x0)], dim=-1)
             outs.append(sample_1d(self.corr_pyramid[i], grid).view(b, h1, w1, -1))
         return torch.cat(outs, dim=-1).permute(0, 3, 1, 2).contiguous().float()
+
+
+def convex_upsample(flow, mask, factor):
+    """RAFT-Stereo's convex upsampler for the mask of model.py:238-241/:264
+    (absent from the reference's forward): softmax over the 9 neighbours,
+    weighted sum of factor * flow over the 3x3 neighbourhood (F.unfold order).
+    Parity of this restatement is unpinned by the reference (no upsampler
+    there); tests/test_upsample.py checks it against an explicit loop."""
+    N, C, H, W = flow.shape
+    m = torch.softmax(mask.view(N, 1, 9, factor, factor, H, W), dim=2)
+    up = F.unfold(factor * flow, [3, 3], padding=1).view(N, C, 9, 1, 1, H, W)
+    up = torch.sum(m * up, dim=2)                       # N, C, f, f, H, W
+    return up.permute(0, 1, 4, 2, 5, 3).reshape(N, C, factor * H, factor * W)

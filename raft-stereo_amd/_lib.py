@@ -34,6 +34,7 @@ SIGNATURES = {
                                  _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "rc_corr_lookup_backward": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l),
                                      _i, _i, _vp, _l, _i, _i, _i, _vp, _vp]),
+    "rc_convex_upsample": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rc_corr_build_backward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_vp),
                                     ctypes.POINTER(_l), _i, _vp, _vp, _vp]),
 }

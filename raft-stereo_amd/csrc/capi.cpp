@@ -340,3 +340,17 @@ extern "C" int rc_corr_lookup_conv(const void *const *pyr, const int *widths, co
                                         out, reinterpret_cast<hipStream_t>(stream)),
                   "rc_corr_lookup_conv: launch");
 }
+
+extern "C" int rc_convex_upsample(const float *flow, const float *mask, int N, int C, int H, int W,
+                                  int factor, float *out, void *stream) {
+    g_err[0] = 0;
+    if (N < 0 || C < 1 || H < 0 || W < 0)
+        return fail(RC_EINVAL, "rc_convex_upsample: bad shape N=%d C=%d H=%d W=%d", N, C, H, W);
+    if (factor != 1 && factor != 2 && factor != 4 && factor != 8)
+        return fail(RC_EUNSUPPORTED, "rc_convex_upsample: factor %d (1, 2, 4 or 8)", factor);
+    if ((long long)N * H * W == 0) return RC_OK;
+    if (!flow || !mask || !out) return fail(RC_EINVAL, "rc_convex_upsample: null pointer");
+    return hip_rc(rc_launch_convex_upsample(flow, mask, N, C, H, W, factor, out,
+                                            reinterpret_cast<hipStream_t>(stream)),
+                  "rc_convex_upsample: launch");
+}

@@ -114,3 +114,5 @@ hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf
 hipError_t rc_launch_lookup_chain(const rc::LookupArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s);
+hipError_t rc_launch_convex_upsample(const float *flow, const float *mask, int N, int C, int H,
+                                     int W, int factor, float *out, hipStream_t s);

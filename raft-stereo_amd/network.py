@@ -276,7 +276,11 @@ class RAFTStereo(nn.Module):
                         for i, conv in zip(inp_list, self.context_zqr_convs)]
         return fmap1, fmap2, net_list, inp_list
 
-    def forward(self, image1, image2, iters=12, flow_init=None, test_mode=False):
+    def forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, upsample=False):
+        """Per-iteration low-resolution flow (the reference's D8 tail), or with
+        ``upsample=True`` the full-resolution x-flow of each iteration through
+        the convex upsampler (``upsample.convex_upsample``)
+        using the update block's mask (model.py:238-241, :264)."""
         a = self.args
         fmap1, fmap2, net_list, inp_list = self.features(image1, image2)
         corr_fn = self.corr_block(fmap1, fmap2, radius=a.corr_radius, num_levels=a.corr_levels)
@@ -287,6 +291,7 @@ class RAFTStereo(nn.Module):
         fused = self.fuse_convc1 and not step and hasattr(corr_fn, "lookup_convc1")
         enc = self.update_block.encoder
         predictions = []
+        masks = []
         delta = None
         for itr in range(iters):
             coords1 = coords1.detach()
@@ -312,6 +317,8 @@ class RAFTStereo(nn.Module):
                 net_list, up_mask, delta_flow = self.update_block(
                     net_list, inp_list, corr, flow, iter32=a.n_gru_layers == 3,
                     iter16=a.n_gru_layers >= 2, corr_is_convc1=fused)
+            if upsample:
+                masks.append(up_mask)
             if step:
                 delta = delta_flow.float()              # applied by the next launch
                 continue
@@ -322,4 +329,8 @@ class RAFTStereo(nn.Module):
             delta[:, 1] = 0.0
             coords1 = coords1 + delta
             predictions.append(coords1 - coords0)
+        if upsample:
+            from .upsample import convex_upsample
+            f = 2 ** a.n_downsample
+            predictions = [convex_upsample(p[:, :1], m, f) for p, m in zip(predictions, masks)]
         return predictions
