@@ -129,7 +129,8 @@ def cpu_baseline(cfg, seconds_target=15.0):
             "sec_per_pair": t}
 
 
-def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False):
+def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False,
+                    fuse_step=False):
     """Whole network (encoders/GRU on PyTorch ops + the HIP corr path) on
     synthetic pairs at the config's image size: pairs/s and the corr share."""
     from raft_stereo_amd.network import RAFTStereo, StereoArgs
@@ -138,7 +139,7 @@ def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False
     args = StereoArgs(corr_levels=L, corr_radius=r, mixed_precision=mixed)
     if mixed:
         args.autocast_dtype = torch.bfloat16
-    model = RAFTStereo(args).eval().to(device)
+    model = RAFTStereo(args, fuse_step=fuse_step).eval().to(device)
     g = torch.Generator().manual_seed(1234)
     H, W = image_hw
     img1 = (torch.rand(B, 3, H, W, generator=g) * 255).to(device)
@@ -153,7 +154,7 @@ def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
     return {"pairs_per_s": B / dt, "ms_per_batch": dt * 1e3, "batch": B, "image": [H, W],
-            "iters": iters, "mixed_precision": mixed,
+            "iters": iters, "mixed_precision": mixed, "fuse_step": fuse_step,
             "note": "full network; encoders/GRU/heads on PyTorch (MIOpen) ops per north_star"}
 
 
@@ -424,6 +425,9 @@ def main():
                    "frac": lgbs / HBM_PEAK_GBS, "traffic": ltraffic,
                    "algorithmic_bytes": lbytes, "kernel": lname,
                    "avg_launch_us": lookup_launch_ms * 1e3}
+    if ltraffic:   # the HBM bytes the kernel really moves (PMC), per second
+        roof_lookup["traffic_gbs"] = ltraffic / (lookup_launch_ms * 1e-3) / 1e9
+        roof_lookup["traffic_frac"] = roof_lookup["traffic_gbs"] / HBM_PEAK_GBS
     dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
 
     result = {
@@ -464,6 +468,13 @@ def main():
         result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1)
         result["e2e"]["pairs_per_s_all_ranks"] = result["e2e"]["pairs_per_s"] * world
         result["e2e"]["corr_path_share"] = (ms_per_step / result["e2e"]["ms_per_batch"])
+    if args.e2e_steps > 0 and args.config == "realtime":
+        # C5 is latency-bound: whole network per pair, with and without the
+        # loop's coords update + flow fused into the lookup
+        result["e2e"] = {
+            "unfused": e2e_pairs_per_s(cfg, device, max(args.e2e_steps, 10), 3, (480, 640)),
+            "fused_step": e2e_pairs_per_s(cfg, device, max(args.e2e_steps, 10), 3, (480, 640),
+                                          fuse_step=True)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
