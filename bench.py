@@ -371,14 +371,22 @@ def main():
             build_ms = sum(e0.elapsed_time(e1) for e0, e1 in be) / len(be)
         # per-launch lookup duration without the host gaps between launches:
         # events around each launch of one extra pass
+        # A device-side sleep first lets the host queue every launch before the
+        # GPU reaches them, so no event pair spans a host gap; median over 3
+        # passes of all launches.
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
-        le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
-        for it in range(iters):
-            le[it][0].record()
-            blk(coords[it])
-            le[it][1].record()
-        torch.cuda.synchronize()
-        lookup_launch_ms = sum(a.elapsed_time(b) for a, b in le) / iters
+        per_launch = []
+        for _ in range(3):
+            le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
+            torch.cuda._sleep(5_000_000)
+            for it in range(iters):
+                le[it][0].record()
+                blk(coords[it])
+                le[it][1].record()
+            torch.cuda.synchronize()
+            per_launch += [a.elapsed_time(b) for a, b in le]
+        per_launch.sort()
+        lookup_launch_ms = per_launch[len(per_launch) // 2]
 
     # per-step latency distribution (p50) for the latency-bound realtime config
     lat = []
@@ -418,7 +426,7 @@ def main():
                        "kernel": "rc::build_f32_ring_kernel<4,0>", "avg_launch_us": build_ms * 1e3,
                        "levels_written": nbuf}
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
-    lname = (f"rc::lookup_chain_kernel<{r},{L}>" if blk._chain
+    lname = (f"rc::lookup_chain_kernel<{r},{L},0>" if blk._chain
              else f"rc::lookup_kernel<{r},0,{'true' if bf16 else 'false'},true>")
     ltraffic = traffic.get("lookup_chain_bytes" if blk._chain else "lookup_bytes")
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

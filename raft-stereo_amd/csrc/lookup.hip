@@ -144,6 +144,10 @@ __device__ __forceinline__ void finish_level(const LevelWindow<R, BF16> &lw, con
         for (int k = 1; k < EPV; ++k) r = (lw.sh == k) ? v[j + k] : r;
         s[j] = r;
     }
+    // fast path for every tap, then ONE wave-level check for the (unreachable
+    // within the error bound) taps whose floor left the window
+    float res[T];
+    bool bad = false;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const float xp = lw.xp[t];
@@ -151,29 +155,40 @@ __device__ __forceinline__ void finish_level(const LevelWindow<R, BF16> &lw, con
         const float w1 = xp - x0, w0 = 1.0f - w1;
         const float nt = lw.n + (float)(t - R);
         const bool lo = x0 < nt, hi = x0 > nt;
-        float a0 = lo ? s[t] : (hi ? s[t + 2] : s[t + 1]);
-        float a1 = lo ? s[t + 1] : (hi ? s[t + 3] : s[t + 2]);
+        const float a0 = lo ? s[t] : (hi ? s[t + 2] : s[t + 1]);
+        const float a1 = lo ? s[t + 1] : (hi ? s[t + 3] : s[t + 2]);
         const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
         const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
-        if (__builtin_expect(lw.inwin && (x0 < nt - 1.0f || x0 > nt + 1.0f), 0)) {
-            // Guarded scalar fallback (never taken within the error bound).
-            const char *base = reinterpret_cast<const char *>(a.lvl[i]) + pblk * a.ld[i] * LW::ES;
-            const long long k0 = lrow * a.ld[i] + (long long)x0;
-            if constexpr (BF16) {
-                const uint16_t *rowp = reinterpret_cast<const uint16_t *>(base);
-                a0 = ok0 ? bf16_to_f32(rowp[k0]) : 0.0f;
-                a1 = ok1 ? bf16_to_f32(rowp[k0 + 1]) : 0.0f;
-            } else {
-                const float *rowp = reinterpret_cast<const float *>(base);
-                a0 = ok0 ? rowp[k0] : 0.0f;
-                a1 = ok1 ? rowp[k0 + 1] : 0.0f;
-            }
-        }
+        bad |= lw.inwin && (x0 < nt - 1.0f || x0 > nt + 1.0f);
         const float v0 = ok0 ? a0 : 0.0f;
         const float v1 = ok1 ? a1 : 0.0f;
-        const float res = fmaf(w1, v1, w0 * v0);
-        sink(t, res);
+        res[t] = fmaf(w1, v1, w0 * v0);
     }
+    if (__builtin_expect(bad, 0)) {
+        // Guarded scalar fallback: re-read every tap of this lane from memory.
+        const char *base = reinterpret_cast<const char *>(a.lvl[i]) + pblk * a.ld[i] * LW::ES;
+        for (int t = 0; t < T; ++t) {
+            const float xp = lw.xp[t];
+            const float x0 = floorf(xp);
+            const float w1 = xp - x0, w0 = 1.0f - w1;
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            const long long k0 = lrow * a.ld[i] + (long long)x0;
+            float v0 = 0.0f, v1 = 0.0f;
+            if constexpr (BF16) {
+                const uint16_t *rowp = reinterpret_cast<const uint16_t *>(base);
+                if (ok0) v0 = bf16_to_f32(rowp[k0]);
+                if (ok1) v1 = bf16_to_f32(rowp[k0 + 1]);
+            } else {
+                const float *rowp = reinterpret_cast<const float *>(base);
+                if (ok0) v0 = rowp[k0];
+                if (ok1) v1 = rowp[k0 + 1];
+            }
+            res[t] = fmaf(w1, v1, w0 * v0);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) sink(t, res[t]);
 }
 
 // NL > 0: compile-time level count (all loads issue first); NL == 0: runtime.
@@ -239,7 +254,10 @@ __device__ __forceinline__ float derived_elem(const float *row1, long long k) {
     return pool_tree<SI>(v);
 }
 
-template <int R, int NL>
+// M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT in launch_chain_r): 0 = product,
+// 1 = no output stores (kept live by an impossible compare), 2 = no pyramid loads,
+// 3 = pyramid loads only (no tap math, no stores), 4 = tap math only.
+template <int R, int NL, int M = 0>
 __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
     static_assert(NL >= 3 && NL <= 4, "chain lookup: 3 or 4 levels");
     constexpr int T = 2 * R + 1, NW = 2 * R + 4, TOP = NL - 1, S = 1 << (TOP - 1);
@@ -257,7 +275,8 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
 
     // level 0: its own window (lookup_kernel's path)
     LevelWindow<R, false> lw0;
-    issue_level<R, false, true>(lw0, a, 0, x, pblk, lrow);
+    constexpr bool NOLOAD = M == 2 || M == 4, NOSTORE = M == 1 || M == 4;
+    issue_level<R, false, true>(lw0, a, 0, NOLOAD ? NAN : x, pblk, lrow);
 
     // levels 1..TOP: one span of level 1, starting at e1 = S (n_top - R - 1)
     const float xtop = x / (float)(1 << TOP);
@@ -290,13 +309,26 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
 #pragma unroll
     for (int k = 0; k < NC1; ++k) {
         const int cs = ea + 4 * k;
-        const bool ok = cs <= hi && cs + 3 >= lo;      // lo >= 0 and hi < W_1: inside the row
+        const bool ok = !NOLOAD && cs <= hi && cs + 3 >= lo;   // lo >= 0 and hi < W_1: inside the row
         q1[k] = ld4(rs1, ok ? (uint32_t)((lrow * ld1 + cs) * 4) : 0xFFFFFF00u);
+    }
+    if constexpr (M == 3) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < LevelWindow<R, false>::NV; ++k)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc ^= lw0.q[k][c];
+#pragma unroll
+        for (int k = 0; k < NC1; ++k)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc ^= __builtin_bit_cast(uint32_t, q1[k][c]);
+        if (acc == 0x12345678u) outp[0] = 0.0f;
+        return;
     }
 
     // level 0 math + stores while the span is in flight
     finish_level<R, false>(lw0, a, 0, pblk, lrow, [&](int t, float v) {
-        if (active) outp[(long long)t * a.HW] = v;
+        if (!NOSTORE || v == 1234.5f) outp[(long long)t * a.HW] = v;
     });
 
     // s1[k] = level-1 element e1 + k
@@ -336,6 +368,8 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
             }
             w[jj] = val;
         }
+        float res[T];
+        bool bad = false;
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const float xt = (float)(t - R) + xl;
@@ -345,35 +379,66 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
             const float w1 = xp - x0, w0 = 1.0f - w1;
             const float nt = n + (float)(t - R);
             const bool lo_ = x0 < nt, hi_ = x0 > nt;
-            float a0 = lo_ ? w[t] : (hi_ ? w[t + 2] : w[t + 1]);
-            float a1 = lo_ ? w[t + 1] : (hi_ ? w[t + 3] : w[t + 2]);
+            const float a0 = lo_ ? w[t] : (hi_ ? w[t + 2] : w[t + 1]);
+            const float a1 = lo_ ? w[t + 1] : (hi_ ? w[t + 3] : w[t + 2]);
             const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
             const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
-            if (__builtin_expect(inwin && (!valid || x0 < nt - 1.0f || x0 > nt + 1.0f), 0)) {
-                a0 = ok0 ? derived_elem<SI>(row1, (long long)x0) : 0.0f;
-                a1 = ok1 ? derived_elem<SI>(row1, (long long)x0 + 1) : 0.0f;
-            }
+            bad |= inwin && (!valid || x0 < nt - 1.0f || x0 > nt + 1.0f);
             const float v0 = ok0 ? a0 : 0.0f;
             const float v1 = ok1 ? a1 : 0.0f;
-            const float res = fmaf(w1, v1, w0 * v0);
-            if (active) outp[(long long)(i * T + t) * a.HW] = res;
+            res[t] = fmaf(w1, v1, w0 * v0);
         }
+        if (__builtin_expect(bad, 0)) {   // one wave-level check per level
+            for (int t = 0; t < T; ++t) {
+                const float xt = (float)(t - R) + xl;
+                const float xn = (2.0f * xt) / Wm1 - 1.0f;
+                const float xp = (xn + 1.0f) * half;
+                const float x0 = floorf(xp);
+                const float w1 = xp - x0, w0 = 1.0f - w1;
+                const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+                const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+                const float v0 = ok0 ? derived_elem<SI>(row1, (long long)x0) : 0.0f;
+                const float v1 = ok1 ? derived_elem<SI>(row1, (long long)x0 + 1) : 0.0f;
+                res[t] = fmaf(w1, v1, w0 * v0);
+            }
+        }
+        // inactive lanes (tail block) hold pixel P-1's values: storing them
+        // again is a same-value write, so the stores need no predicate
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+            if (!NOSTORE || res[t] == 1234.5f) outp[(long long)(i * T + t) * a.HW] = res[t];
     };
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
     if constexpr (TOP >= 3) level(std::integral_constant<int, 3>{});
 }
 
-template <int R>
-static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
+template <int R, int M>
+static hipError_t launch_chain_m(const LookupArgs &a, hipStream_t s, unsigned lds = 0) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
     if (a.levels == 4)
-        hipLaunchKernelGGL((lookup_chain_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((lookup_chain_kernel<R, 4, M>), dim3(nblk), dim3(256), lds, s, a);
     else if (a.levels == 3)
-        hipLaunchKernelGGL((lookup_chain_kernel<R, 3>), dim3(nblk), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((lookup_chain_kernel<R, 3, M>), dim3(nblk), dim3(256), lds, s, a);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+template <int R>
+static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
+    int variant = 0;
+    if (const char *e = getenv("RAFTCORR_LOOKUP_VARIANT")) variant = atoi(e);
+    if constexpr (R == 4) {   // ablation variants (dev-only), config-2 radius
+        if (variant == 101) return launch_chain_m<R, 1>(a, s);
+        if (variant == 102) return launch_chain_m<R, 2>(a, s);
+        if (variant == 103) return launch_chain_m<R, 3>(a, s);
+        if (variant == 104) return launch_chain_m<R, 4>(a, s);
+        // occupancy caps through reserved LDS: 2 / 3 blocks per CU
+        if (variant == 105) return launch_chain_m<R, 0>(a, s, 64 << 10);
+        if (variant == 106) return launch_chain_m<R, 0>(a, s, 48 << 10);
+    }
+    return launch_chain_m<R, 0>(a, s);
 }
 
 // ---- lookup fused with the motion encoder's convc1 (+ ReLU) ----

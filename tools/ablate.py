@@ -23,6 +23,7 @@ from raft_stereo_amd import corr as rcorr  # noqa: E402
 
 def time_launches(fn, n):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    torch.cuda._sleep(2_000_000)   # let the host queue all n launches first
     ev[0].record()
     for k in range(n):
         fn()
@@ -92,6 +93,11 @@ def main():
                 res.setdefault("lookup_chain", []).extend(t)
                 t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, c, L, r), 8)
                 res.setdefault("lookup_perlevel", []).extend(t)
+                for v in (101, 102, 103, 104, 105, 106):   # chain ablations: no stores / no loads / loads only / math only
+                    os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
+                    t = time_launches(lambda: rcorr.lookup_chain(ref_blk.corr_pyramid, c, L, r), 8)
+                    res.setdefault(f"lookup_chain_v{v}", []).extend(t)
+                os.environ["RAFTCORR_LOOKUP_VARIANT"] = "0"
         if a.bwd:
             P = B * H * W1
             widths = [W2 >> i for i in range(L)]

@@ -23,12 +23,12 @@ step() {  # step <name> <timeout> cmd...
     return 0
 }
 rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
-has test  && step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
+has test  && step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has bench && step bench 600 python bench.py
 has e2e && step e2e_probe 900 python tools/e2e_probe.py
 has probe && step line_probe 300 python tools/line_probe.py
-has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain --convc1
+has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
 has ablatek && step ablate_kitti 600 python tools/ablate.py --config kitti --build-modes 0,2,1,3 --lookup-variants 0,1,3
 has configs && step bench_realtime 300 python bench.py --config realtime --no-cpu-baseline --steps 50 --warmup 5 && step bench_realtime_graph 300 python bench.py --config realtime --graph --no-cpu-baseline --steps 200 --warmup 10
 has configs && step bench_middlebury 300 python bench.py --config middlebury --no-cpu-baseline --steps 5 --warmup 2
