@@ -51,6 +51,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(LookupBwdArgs a) {
     for (int i = 0; i < a.levels; ++i) {
         const int W = a.W[i];
         const float Wm1 = (float)(W - 1);
+        const DivRN dv = div_prep(Wm1);
         const float half = Wm1 / 2.0f;
         const float xl = x / (float)(1 << i);
         const bool inwin = (xl > -(float)(R + 4)) && (xl < (float)(W + R + 4));  // false for NaN
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(LookupBwdArgs a) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const float xt = (float)(t - R) + xl;
-            const float xn = (2.0f * xt) / Wm1 - 1.0f;       // model.py:271
+            const float xn = div_rn(2.0f * xt, dv) - 1.0f;       // model.py:271
             const float xp = (xn + 1.0f) * half;              // :275 unnormalise
             const float x0 = floorf(xp);
             const float w1 = xp - x0, w0 = (x0 + 1.0f) - xp;  // ne / nw corner weights

@@ -10,6 +10,30 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kMaxLevels = 8;
 
+// Correctly rounded a / b for the sampler's normalisation xn = 2x/(W-1) - 1
+// (model.py:271), with b = W - 1 a positive integer.  rb = RN(1/b) is computed
+// once per level; per tap Markstein's correction q0 = RN(a*rb) (within 1 ulp
+// of a/b), r = a - q0*b (exact with fma), q = RN(q0 + r*rb) = RN(a/b)
+// (Markstein, IBM J. R&D 34(1), 1990; Muller et al., Handbook of
+// Floating-Point Arithmetic, ch. 4) costs 3 VALU ops instead of the ~10-op
+// IEEE division sequence with its quarter-rate v_rcp.  tests/test_div_rn.py
+// checks it bit for bit against IEEE division on gfx950 for EVERY b in
+// [1, 8192] and every fp32 a with 2^-30 <= |a| < 2^15, and for sampled wider
+// b.  Outside that a-range a difference could not reach the sampler's output:
+// |a| < 2^-30 gives |q| < 2^-25, so xn = q - 1 rounds to -1 either way, and
+// |a| > 2(W + R + 2) puts every tap outside the row (zeros).  A NaN/inf
+// numerator gives NaN where division gives +-inf; the sampler turns both into
+// the same NaN output (W = 1, b = 0, likewise: (xn + 1) * 0 is NaN both ways).
+struct DivRN {
+    float b, rb;
+};
+__device__ __forceinline__ DivRN div_prep(float b) { return DivRN{b, 1.0f / b}; }
+__device__ __forceinline__ float div_rn(float a, const DivRN &d) {
+    const float q0 = a * d.rb;
+    const float r = __builtin_fmaf(-q0, d.b, a);
+    return __builtin_fmaf(r, d.rb, q0);
+}
+
 // Raw buffer resource over [base, base + bytes): loads past the end (or at a
 // "negative" offset, which wraps to a huge unsigned one) return 0 and never
 // fault.  Build it from wave-uniform values only (cdna_hip_programming.md T20).

@@ -81,12 +81,13 @@ __device__ __forceinline__ void issue_level(LevelWindow<R, BF16> &lw, const Look
     const int W = a.W[i];
     const long long ld = a.ld[i];
     const float Wm1 = (float)(W - 1);
+    const DivRN dv = div_prep(Wm1);
     const float half = Wm1 / 2.0f;
     const float xl = x / (float)(1 << i);
 #pragma unroll
     for (int t = 0; t < LW::T; ++t) {
         const float xt = (float)(t - R) + xl;
-        const float xn = (2.0f * xt) / Wm1 - 1.0f;
+        const float xn = div_rn(2.0f * xt, dv) - 1.0f;
         lw.xp[t] = (xn + 1.0f) * half;
     }
     lw.inwin = (xl > -(float)(R + 4)) && (xl < (float)(W + R + 4));  // false for NaN
@@ -290,10 +291,11 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
 #pragma unroll
         for (int i = 1; i <= TOP; ++i) {
             const float Wm1 = (float)(a.W[i] - 1), half = Wm1 / 2.0f;
+            const DivRN dv = div_prep(Wm1);
             const float xl = x / (float)(1 << i);
             const float xa = (float)(-R) + xl, xb = (float)R + xl;
-            const float pa = ((2.0f * xa) / Wm1 - 1.0f + 1.0f) * half;
-            const float pb = ((2.0f * xb) / Wm1 - 1.0f + 1.0f) * half;
+            const float pa = ((div_rn(2.0f * xa, dv) - 1.0f) + 1.0f) * half;
+            const float pb = ((div_rn(2.0f * xb, dv) - 1.0f) + 1.0f) * half;
             const int f = max((int)floorf(pa), 0);
             const int l = min((int)floorf(pb) + 1, a.W[i] - 1);
             if (f <= l) {
@@ -348,6 +350,7 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
         constexpr int SI = 1 << (i - 1), NDD = 1 << (TOP - i);
         const int W = a.W[i];
         const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+        const DivRN dv = div_prep(Wm1);
         const float xl = x / (float)(1 << i);
         const float n = inwin ? floorf(xl) : 0.0f;
         // n = NDD * n_top + dd, dd in [0, NDD) (x / 2^i is exact); a subnormal
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const float xt = (float)(t - R) + xl;
-            const float xn = (2.0f * xt) / Wm1 - 1.0f;
+            const float xn = div_rn(2.0f * xt, dv) - 1.0f;
             const float xp = (xn + 1.0f) * half;
             const float x0 = floorf(xp);
             const float w1 = xp - x0, w0 = 1.0f - w1;
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
         if (__builtin_expect(bad, 0)) {   // one wave-level check per level
             for (int t = 0; t < T; ++t) {
                 const float xt = (float)(t - R) + xl;
-                const float xn = (2.0f * xt) / Wm1 - 1.0f;
+                const float xn = div_rn(2.0f * xt, dv) - 1.0f;
                 const float xp = (xn + 1.0f) * half;
                 const float x0 = floorf(xp);
                 const float w1 = xp - x0, w0 = 1.0f - w1;

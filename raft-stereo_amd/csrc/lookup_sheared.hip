@@ -45,12 +45,13 @@ __device__ __forceinline__ void shear_issue(ShearWindow<R> &sw, const ShearArgs 
     constexpr int T = ShearWindow<R>::T, NW = ShearWindow<R>::NW;
     const int W = a.W[i];
     const float Wm1 = (float)(W - 1);
+    const DivRN dv = div_prep(Wm1);
     const float half = Wm1 / 2.0f;
     const float xl = x / (float)(1 << i);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const float xt = (float)(t - R) + xl;
-        const float xn = (2.0f * xt) / Wm1 - 1.0f;
+        const float xn = div_rn(2.0f * xt, dv) - 1.0f;
         sw.xp[t] = (xn + 1.0f) * half;
     }
     sw.inwin = (xl > -(float)(R + 4)) && (xl < (float)(W + R + 4));
