@@ -437,9 +437,6 @@ static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
         if (variant == 102) return launch_chain_m<R, 2>(a, s);
         if (variant == 103) return launch_chain_m<R, 3>(a, s);
         if (variant == 104) return launch_chain_m<R, 4>(a, s);
-        // occupancy caps through reserved LDS: 2 / 3 blocks per CU
-        if (variant == 105) return launch_chain_m<R, 0>(a, s, 64 << 10);
-        if (variant == 106) return launch_chain_m<R, 0>(a, s, 48 << 10);
     }
     return launch_chain_m<R, 0>(a, s);
 }
