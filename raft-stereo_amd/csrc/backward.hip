@@ -123,6 +123,152 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(LookupBwdArgs a) {
     }
 }
 
+// lookup_bwd_pre_kernel -- the same arithmetic as lookup_bwd_kernel, with the
+// level count fixed at compile time so that every load of the launch issues
+// before any tap math: all NL*(2r+1) output-gradient values, then, per level,
+// the 16-byte chunks of the gradient row that intersect the lane's register
+// window [n-R-1, n+R+2] clipped to [0, W).  (lookup_bwd_kernel waits on each
+// level's read-modify-write chunks in turn, so the wave pays the load latency
+// NL times.)  Every element a tap touches lies in that window (x0 is within
+// one of the tap's nominal index nt), so a touched chunk is always loaded; only
+// touched chunks are stored.  A lane with an out-of-window tap (unreachable
+// within the division's error bound, kept for exactness) applies those direct
+// updates first and reloads its chunks, in lookup_bwd_kernel's order, so the
+// results are bit-identical to it.
+template <int R, int NL, int WPE = 1, int PF = 8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_bwd_pre_kernel(LookupBwdArgs a) {
+    constexpr int T = 2 * R + 1, NW = 2 * R + 4, NV = (NW + 6) / 4;
+    const long long pblk = (long long)blockIdx.x * 256;
+    const long long p = pblk + threadIdx.x;
+    if (p >= a.P) return;   // no barriers in this kernel
+    const long long lrow = p - pblk;
+    const long long bimg = p / a.HW, rem = p - bimg * a.HW;
+    const float x = a.coords[bimg * a.cbs + rem];
+    const float *go = a.grad_out + bimg * (long long)(NL * T) * a.HW + rem;
+
+    float gv[NL][T];
+    f32x4 v[NL][NV];
+    float nn[NL];
+    bool win[NL];
+    // issue(i): level i's output-gradient values and gradient-row chunks
+    auto issue = [&](int i) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) gv[i][t] = go[(long long)(i * T + t) * a.HW];
+        const int W = a.W[i];
+        const float xl = x / (float)(1 << i);
+        win[i] = (xl > -(float)(R + 4)) && (xl < (float)(W + R + 4));   // false for NaN
+        nn[i] = win[i] ? floorf(xl) : 0.0f;
+        const int e0 = (int)nn[i] - R - 1;
+        const int ea = e0 & ~3;
+        const int wlo = max(e0, 0), whi = min(e0 + NW - 1, W - 1);
+        // block-uniform resource over this block's rows; a skipped chunk gets
+        // an out-of-range offset (reads 0, no fault)
+        const long long ld = a.ld[i];
+        const auto rs = make_rsrc(a.g[i] + pblk * ld, clamp_bytes((a.P - pblk) * ld * 4));
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int cs = ea + 4 * k;
+            // cs >= 0 and cs <= W - 1 < ld: the chunk is inside the lane's row
+            const bool ok = win[i] && cs <= whi && cs + 3 >= wlo;
+            v[i][k] = ld4(rs, ok ? (uint32_t)((lrow * ld + cs) * 4) : 0xFFFFFF00u);
+        }
+    };
+    // PF levels in flight ahead of the one being computed (PF >= NL: all up front)
+#pragma unroll
+    for (int i = 0; i < (PF < NL ? PF : NL); ++i) issue(i);
+
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        if (i + PF < NL) issue(i + PF);
+        const int W = a.W[i];
+        const float Wm1 = (float)(W - 1);
+        const DivRN dv = div_prep(Wm1);
+        const float half = Wm1 / 2.0f;
+        const float xl = x / (float)(1 << i);
+        const bool inwin = win[i];
+        const float n = nn[i];
+        float *row = a.g[i] + p * a.ld[i];
+        float acc[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) acc[j] = 0.0f;
+        int first = 0x7FFFFFFF, last = -1;
+        bool bad = false;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + xl;
+            const float xn = div_rn(2.0f * xt, dv) - 1.0f;       // model.py:271
+            const float xp = (xn + 1.0f) * half;              // :275 unnormalise
+            const float x0 = floorf(xp);
+            const float w1 = xp - x0, w0 = (x0 + 1.0f) - xp;
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            const float c0 = w0 * gv[i][t], c1 = w1 * gv[i][t];
+            const float nt = n + (float)(t - R);
+            const bool out = !inwin || x0 < nt - 1.0f || x0 > nt + 1.0f;
+            bad |= out && (ok0 || ok1);
+            const int j0 = t + (x0 < nt ? 0 : (x0 > nt ? 2 : 1));
+            const int e = (int)x0;
+            const bool u0 = ok0 && !out, u1 = ok1 && !out;
+            if (u0) { first = min(first, e); last = max(last, e); }
+            if (u1) { first = min(first, e + 1); last = max(last, e + 1); }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = t + q;
+                if (j < NW) {
+                    float add = acc[j];
+                    if (u0 && j0 == j) add += c0;
+                    if (u1 && j0 + 1 == j) add += c1;
+                    acc[j] = add;
+                }
+            }
+        }
+        const int e0 = (int)n - R - 1;
+        const int ea = e0 & ~3;
+        const int sh = e0 - ea;
+        if (__builtin_expect(bad, 0)) {
+            // lookup_bwd_kernel's order: direct updates first (tap order), then
+            // the window's read-modify-write on fresh chunk values
+            for (int t = 0; t < T; ++t) {
+                const float xt = (float)(t - R) + xl;
+                const float xn = div_rn(2.0f * xt, dv) - 1.0f;
+                const float xp = (xn + 1.0f) * half;
+                const float x0 = floorf(xp);
+                const float w1 = xp - x0, w0 = (x0 + 1.0f) - xp;
+                const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+                const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+                const float nt = n + (float)(t - R);
+                if (!inwin || x0 < nt - 1.0f || x0 > nt + 1.0f) {
+                    if (ok0) row[(long long)x0] += w0 * gv[i][t];
+                    if (ok1) row[(long long)x0 + 1] += w1 * gv[i][t];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                const int cs = ea + 4 * k;
+                if (!(cs > last || cs + 3 < first)) v[i][k] = *reinterpret_cast<const f32x4 *>(row + cs);
+            }
+        }
+        if (last < first) continue;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int cs = ea + 4 * k;
+            if (cs > last || cs + 3 < first) continue;
+            f32x4 w = v[i][k];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float add = 0.0f;   // acc[4k + c - sh]
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int j = 4 * k + c - s;
+                    if (j >= 0 && j < NW) add = (sh == s) ? acc[j] : add;
+                }
+                w[c] += add;
+            }
+            *reinterpret_cast<f32x4 *>(row + cs) = w;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- volume bwd
 
 // Reduction elements per stage KS = 32 (LDS rows of 40 floats) or 16 (rows
@@ -335,6 +481,33 @@ void volume_bwd_kernel(BuildBwdArgs a, int nwg_total) {
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    // dev-only A/B: RAFTCORR_LOOKUP_BWD_VARIANT=1 forces the per-level-wait kernel
+    int variant = 0;
+    if (const char *e = getenv("RAFTCORR_LOOKUP_BWD_VARIANT")) variant = atoi(e);
+    if (variant >= 3 && variant <= 5 && radius == 4 && a.levels == 4) {
+        // 3: occupancy cap 3 waves/SIMD; 4 / 5: one / two levels prefetched ahead
+        if (variant == 3) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
+        if (variant == 4) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 1>), dim3(nblk), dim3(256), 0, s, a);
+        if (variant == 5) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 2>), dim3(nblk), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (variant == 0 && radius >= 1 && radius <= 4 && a.levels >= 1 && a.levels <= 4) {
+#define RC_LBWD(RR)                                                                                      \
+    switch (a.levels) {                                                                                  \
+        case 1: hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<RR, 1>), dim3(nblk), dim3(256), 0, s, a); break; \
+        case 2: hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<RR, 2>), dim3(nblk), dim3(256), 0, s, a); break; \
+        case 3: hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<RR, 3>), dim3(nblk), dim3(256), 0, s, a); break; \
+        default: hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<RR, 4>), dim3(nblk), dim3(256), 0, s, a); break; \
+    }
+        switch (radius) {
+            case 1: RC_LBWD(1) break;
+            case 2: RC_LBWD(2) break;
+            case 3: RC_LBWD(3) break;
+            default: RC_LBWD(4) break;
+        }
+#undef RC_LBWD
+        return hipGetLastError();
+    }
     switch (radius) {
         case 1: hipLaunchKernelGGL(rc::lookup_bwd_kernel<1>, dim3(nblk), dim3(256), 0, s, a); break;
         case 2: hipLaunchKernelGGL(rc::lookup_bwd_kernel<2>, dim3(nblk), dim3(256), 0, s, a); break;

@@ -104,6 +104,40 @@ def test_lookup_backward_levels_vs_oracle(path):
         assert torch.count_nonzero(full[:, grads[i].shape[1]:]) == 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,r,W2", [(4, 4, 240), (3, 4, 311), (4, 3, 70), (2, 2, 33), (1, 1, 16),
+                                    (4, 1, 37)])
+def test_lookup_backward_prefetch_kernel_bit_identical(L, r, W2, monkeypatch):
+    """lookup_bwd_pre_kernel (all loads up front) vs lookup_bwd_kernel (per-level
+    waits, RAFTCORR_LOOKUP_BWD_VARIANT=1): same accumulation, bit for bit,
+    including NaN / inf / far out-of-range coordinates."""
+    from raft_stereo_amd import corr as rcorr
+    g = torch.Generator().manual_seed(L * 100 + r * 10 + W2)
+    B, H, W1 = 2, 3, 57
+    widths = [W2 >> i for i in range(L)]
+    cs, gs = [], []
+    for _ in range(3):
+        x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 48
+        x[..., ::5] = torch.randint(-20, W2 + 20, x[..., ::5].shape, generator=g).float()
+        x[0, 0, 0, :6] = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e30, -1e30, 1e-40])
+        cs.append(torch.cat([x, torch.randn(B, 1, H, W1, generator=g)], 1).to(DEV))
+        gs.append(torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(DEV))
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("RAFTCORR_LOOKUP_BWD_VARIANT", v)
+        grads = rcorr.grad_buffers(B * H * W1, widths, torch.device(DEV))
+        for c, go in zip(cs, gs):
+            rcorr.lookup_backward(grads, c, go, L, r)
+        torch.cuda.synchronize()
+        out[v] = grads
+    for i in range(L):
+        a0 = torch.as_strided(out["0"][i], (out["0"][i].shape[0], out["0"][i].stride(0)),
+                              (out["0"][i].stride(0), 1))
+        a1 = torch.as_strided(out["1"][i], (out["1"][i].shape[0], out["1"][i].stride(0)),
+                              (out["1"][i].stride(0), 1))
+        assert torch.equal(a0, a1), f"level {i}"
+
+
 SHAPES = [
     # B, D, H, W1, W2, L, r, calls
     (2, 256, 3, 240, 240, 4, 4, 3),     # config-2 row width

@@ -43,6 +43,8 @@ def main():
                     help="time rc_corr_lookup_chain vs the per-level rc_corr_lookup")
     ap.add_argument("--bwd", action="store_true",
                     help="time the backward kernels")
+    ap.add_argument("--bwd-variants", default="0,1,3,4,5",
+                    help="RAFTCORR_LOOKUP_BWD_VARIANT values (0 product, 1 per-level waits, 3 capped occupancy, 4/5 prefetch 1/2 levels ahead)")
     ap.add_argument("--convc1", action="store_true",
                     help="also time lookup+convc1+relu fused vs separate (MIOpen 1x1 conv)")
     a = ap.parse_args()
@@ -104,10 +106,26 @@ def main():
             g = torch.Generator().manual_seed(9)
             go = torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev)
             gper = rcorr.grad_buffers(P, widths, dev)
+            bv = [int(x) for x in a.bwd_variants.split(",") if x]
+            # bit-identity of the variants: same accumulation from the same start
+            outs = {}
+            for v in bv:
+                os.environ["RAFTCORR_LOOKUP_BWD_VARIANT"] = str(v)
+                gv = rcorr.grad_buffers(P, widths, dev)
+                for k in range(3):
+                    rcorr.lookup_backward(gv, coords[k], go, L, r)
+                outs[v] = gv
+            for v in bv[1:]:
+                for i in range(L):
+                    assert torch.equal(outs[v][i], outs[bv[0]][i]), ("bwd variant", v, i)
+            del outs
             for rnd in range(a.rounds):
                 c = coords[rnd % iters]
-                t = time_launches(lambda: rcorr.lookup_backward(gper, c, go, L, r), 8)
-                res.setdefault("lookup_bwd", []).extend(t)
+                for v in bv:
+                    os.environ["RAFTCORR_LOOKUP_BWD_VARIANT"] = str(v)
+                    t = time_launches(lambda: rcorr.lookup_backward(gper, c, go, L, r), 8)
+                    res.setdefault(f"lookup_bwd_v{v}", []).extend(t)
+                os.environ["RAFTCORR_LOOKUP_BWD_VARIANT"] = "0"
                 t = time_launches(lambda: rcorr.build_backward(f1, f2, gper), 2)
                 res.setdefault("volume_bwd", []).extend(t)
         if a.convc1:

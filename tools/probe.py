@@ -4,7 +4,8 @@
 
 Launches, in order: a calibration copy (torch clone of a 1 GiB fp32 tensor:
 exactly 1 GiB read + 1 GiB written), N builds (rc::build_f32_ring_kernel), N
-CorrBlock1D lookups (rc::lookup_chain_kernel) and N per-level lookups (rc::lookup_kernel) of bench.py's workload.  tools/pmc_traffic.py turns
+CorrBlock1D lookups (rc::lookup_chain_kernel) and N per-level lookups (rc::lookup_kernel) and N lookup backwards
+(rc::lookup_bwd_pre_kernel) of bench.py's workload.  tools/pmc_traffic.py turns
 the per-dispatch FETCH_SIZE / WRITE_SIZE into bytes per launch.
 """
 import argparse
@@ -42,6 +43,12 @@ def main():
             blk(coords[it % iters])        # rc::lookup_chain_kernel (fp32) / lookup_kernel
         for it in range(a.iters):          # the per-level kernel on the same pyramid
             rcorr.lookup(blk.corr_pyramid, coords[it % iters], L, r)
+        if pdt == torch.float32:           # rc::lookup_bwd_pre_kernel (one per lookup call)
+            P = B * H * W1
+            grads = rcorr.grad_buffers(P, [W2 >> i for i in range(L)], dev)
+            go = torch.randn(B, L * (2 * r + 1), H, W1, device=dev)
+            for it in range(a.iters):
+                rcorr.lookup_backward(grads, coords[it % iters], go, L, r)
         torch.cuda.synchronize()
     print("probe done")
 
