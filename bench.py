@@ -220,7 +220,8 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": lbytes / (lb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                     "algorithmic_bytes": lbytes,
-                                    "kernel": f"rc::lookup_bwd_kernel<{r}>"},
+                                    "kernel": (f"rc::lookup_bwd_pre_kernel<{r},{L}>" if r <= 4 and L <= 4
+                                               else f"rc::lookup_bwd_kernel<{r}>")},
             "note": "step = CorrBlock1D build + lookups + autograd backward to both fmaps "
                     "(random output gradients); kernel times are medians of event-timed launches"}
 
@@ -471,6 +472,12 @@ def main():
     }
     if not args.no_backward and args.config == "sceneflow":
         result["backward"] = backward_timing(cfg, f1, f2, coords)
+        lbt = traffic.get("lookup_bwd_bytes")
+        if lbt:   # PMC bytes the lookup backward really moves, per launch
+            rl = result["backward"]["roofline_lookup_bwd"]
+            rl["traffic"] = lbt
+            rl["traffic_gbs"] = lbt / (result["backward"]["lookup_bwd_us"] * 1e-6) / 1e9
+            rl["traffic_frac"] = rl["traffic_gbs"] / HBM_PEAK_GBS
         result["upsample"] = upsample_timing(cfg, device)
     if args.e2e_steps > 0 and args.config == "sceneflow":
         result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1)
