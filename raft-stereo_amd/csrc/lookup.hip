@@ -257,7 +257,8 @@ __device__ __forceinline__ float derived_elem(const float *row1, long long k) {
 
 // M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT in launch_chain_r): 0 = product,
 // 1 = no output stores (kept live by an impossible compare), 2 = no pyramid loads,
-// 3 = pyramid loads only (no tap math, no stores), 4 = tap math only.
+// 3 = pyramid loads only (no tap math, no stores), 4 = tap math only,
+// 5 = the product with non-temporal output stores.
 template <int R, int NL, int M = 0>
 __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
     static_assert(NL >= 3 && NL <= 4, "chain lookup: 3 or 4 levels");
@@ -330,7 +331,8 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
 
     // level 0 math + stores while the span is in flight
     finish_level<R, false>(lw0, a, 0, pblk, lrow, [&](int t, float v) {
-        if (!NOSTORE || v == 1234.5f) outp[(long long)t * a.HW] = v;
+        if constexpr (M == 5) __builtin_nontemporal_store(v, outp + (long long)t * a.HW);
+        else if (!NOSTORE || v == 1234.5f) outp[(long long)t * a.HW] = v;
     });
 
     // s1[k] = level-1 element e1 + k
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
         // again is a same-value write, so the stores need no predicate
 #pragma unroll
         for (int t = 0; t < T; ++t)
-            if (!NOSTORE || res[t] == 1234.5f) outp[(long long)(i * T + t) * a.HW] = res[t];
+            if constexpr (M == 5) __builtin_nontemporal_store(res[t], outp + (long long)(i * T + t) * a.HW);
+            else if (!NOSTORE || res[t] == 1234.5f) outp[(long long)(i * T + t) * a.HW] = res[t];
     };
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
@@ -437,6 +440,7 @@ static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
         if (variant == 102) return launch_chain_m<R, 2>(a, s);
         if (variant == 103) return launch_chain_m<R, 3>(a, s);
         if (variant == 104) return launch_chain_m<R, 4>(a, s);
+        if (variant == 105) return launch_chain_m<R, 5>(a, s);   // non-temporal output stores
     }
     return launch_chain_m<R, 0>(a, s);
 }

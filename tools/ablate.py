@@ -89,13 +89,16 @@ def main():
                 t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, coords[rnd % iters], L, r), 8)
                 res.setdefault(f"lookup_v{v}", []).extend(t)
         if a.chain:
+            os.environ["RAFTCORR_LOOKUP_VARIANT"] = "105"   # non-temporal stores: same values
+            assert torch.equal(rcorr.lookup_chain(ref_blk.corr_pyramid, coords[0], L, r), ref_out)
+            os.environ["RAFTCORR_LOOKUP_VARIANT"] = "0"
             for rnd in range(a.rounds):
                 c = coords[rnd % iters]
                 t = time_launches(lambda: rcorr.lookup_chain(ref_blk.corr_pyramid, c, L, r), 8)
                 res.setdefault("lookup_chain", []).extend(t)
                 t = time_launches(lambda: rcorr.lookup(ref_blk.corr_pyramid, c, L, r), 8)
                 res.setdefault("lookup_perlevel", []).extend(t)
-                for v in (101, 102, 103, 104):   # chain ablations: no stores / no loads / loads only / math only
+                for v in (101, 102, 103, 104, 105):   # no stores / no loads / loads only / math only / NT stores
                     os.environ["RAFTCORR_LOOKUP_VARIANT"] = str(v)
                     t = time_launches(lambda: rcorr.lookup_chain(ref_blk.corr_pyramid, c, L, r), 8)
                     res.setdefault(f"lookup_chain_v{v}", []).extend(t)
