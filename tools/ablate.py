@@ -131,6 +131,9 @@ def main():
                 os.environ["RAFTCORR_LOOKUP_BWD_VARIANT"] = "0"
                 t = time_launches(lambda: rcorr.build_backward(f1, f2, gper), 2)
                 res.setdefault("volume_bwd", []).extend(t)
+                for nl in (1, 2):   # fewer levels to fold on load (what a pre-folded G would cost)
+                    t = time_launches(lambda: rcorr.build_backward(f1, f2, gper[:nl]), 2)
+                    res.setdefault(f"volume_bwd_nlev{nl}", []).extend(t)
         if a.convc1:
             conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1).to(dev)
             for rnd in range(a.rounds):
