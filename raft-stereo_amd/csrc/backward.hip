@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(LookupBwdArgs a) {
 // within the division's error bound, kept for exactness) applies those direct
 // updates first and reloads its chunks, in lookup_bwd_kernel's order, so the
 // results are bit-identical to it.
-template <int R, int NL, int WPE = 1, int PF = 8>
+template <int R, int NL, int WPE = 1, int PF = 8, bool GVL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_bwd_pre_kernel(LookupBwdArgs a) {
     constexpr int T = 2 * R + 1, NW = 2 * R + 4, NV = (NW + 6) / 4;
     const long long pblk = (long long)blockIdx.x * 256;
@@ -152,8 +152,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     bool win[NL];
     // issue(i): level i's output-gradient values and gradient-row chunks
     auto issue = [&](int i) {
+        if constexpr (!GVL) {
 #pragma unroll
-        for (int t = 0; t < T; ++t) gv[i][t] = go[(long long)(i * T + t) * a.HW];
+            for (int t = 0; t < T; ++t) gv[i][t] = go[(long long)(i * T + t) * a.HW];
+        }
         const int W = a.W[i];
         const float xl = x / (float)(1 << i);
         win[i] = (xl > -(float)(R + 4)) && (xl < (float)(W + R + 4));   // false for NaN
@@ -180,6 +182,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
         if (i + PF < NL) issue(i + PF);
+        if constexpr (GVL) {   // output gradients loaded at their level (fewer live registers)
+#pragma unroll
+            for (int t = 0; t < T; ++t) gv[i][t] = go[(long long)(i * T + t) * a.HW];
+        }
         const int W = a.W[i];
         const float Wm1 = (float)(W - 1);
         const DivRN dv = div_prep(Wm1);
@@ -484,7 +490,9 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
     // dev-only A/B: RAFTCORR_LOOKUP_BWD_VARIANT=1 forces the per-level-wait kernel
     int variant = 0;
     if (const char *e = getenv("RAFTCORR_LOOKUP_BWD_VARIANT")) variant = atoi(e);
-    if (variant >= 3 && variant <= 5 && radius == 4 && a.levels == 4) {
+    if (variant >= 3 && variant <= 6 && radius == 4 && a.levels == 4) {
+        // 6: chunks up front, output gradients loaded per level
+        if (variant == 6) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 8, true>), dim3(nblk), dim3(256), 0, s, a);
         // 3: occupancy cap 3 waves/SIMD; 4 / 5: one / two levels prefetched ahead
         if (variant == 3) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
         if (variant == 4) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 1>), dim3(nblk), dim3(256), 0, s, a);
