@@ -374,6 +374,27 @@ def test_lookup_convc1_vs_separate(L, r, pyr_dt, bias, relu):
     assert norm_err(fused.cpu().numpy(), ref.cpu().numpy()) <= 1e-5
 
 
+def test_lookup_convc1_prefetch_bit_identical(monkeypatch):
+    """The default fused kernel issues every level's loads up front; the
+    one-level-at-a-time kernel (RAFTCORR_CONV_VARIANT=1) does the same
+    arithmetic: identical bits, NaN / inf / out-of-range coords included."""
+    g = torch.Generator().manual_seed(4242)
+    B, D, H, W1, W2, L, r = 2, 32, 3, 130, 130, 4, 4
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 60
+    x[..., ::7] = torch.randint(-20, W2 + 20, x[..., ::7].shape, generator=g).float()
+    x[0, 0, 0, :5] = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e30, -1e30])
+    coords = torch.cat([x, torch.zeros_like(x)], 1).to(DEV)
+    conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1).to(DEV)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        a = blk.lookup_convc1(coords, conv.weight, conv.bias)
+        monkeypatch.setenv("RAFTCORR_CONV_VARIANT", "1")
+        b = blk.lookup_convc1(coords, conv.weight, conv.bias)
+    assert torch.equal(a.nan_to_num(nan=7.0), b.nan_to_num(nan=7.0))
+
+
 @pytest.mark.parametrize("shape", [(2, 64, 3, 240, 240, 4, 4), (1, 32, 2, 311, 311, 3, 3),
                                    (1, 16, 2, 45, 61, 4, 2)], ids=lambda s: "x".join(map(str, s)))
 def test_lazy_levels_equal_fused_epilogue(shape):

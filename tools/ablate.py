@@ -136,10 +136,18 @@ def main():
                     res.setdefault(f"volume_bwd_nlev{nl}", []).extend(t)
         if a.convc1:
             conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1).to(dev)
+            base = ref_blk.lookup_convc1(coords[0], conv.weight, conv.bias)
+            os.environ["RAFTCORR_CONV_VARIANT"] = "1"   # one level at a time: same values
+            assert torch.equal(ref_blk.lookup_convc1(coords[0], conv.weight, conv.bias), base)
+            os.environ["RAFTCORR_CONV_VARIANT"] = "0"
             for rnd in range(a.rounds):
                 c = coords[rnd % iters]
                 t = time_launches(lambda: ref_blk.lookup_convc1(c, conv.weight, conv.bias), 8)
                 res.setdefault("convc1_fused", []).extend(t)
+                os.environ["RAFTCORR_CONV_VARIANT"] = "1"
+                t = time_launches(lambda: ref_blk.lookup_convc1(c, conv.weight, conv.bias), 8)
+                res.setdefault("convc1_fused_perlevel", []).extend(t)
+                os.environ["RAFTCORR_CONV_VARIANT"] = "0"
                 t = time_launches(lambda: torch.relu(conv(ref_blk(c))), 8)
                 res.setdefault("convc1_separate", []).extend(t)
     out = {k: {"median_us": statistics.median(v), "min_us": min(v), "n": len(v)} for k, v in res.items()}

@@ -30,6 +30,7 @@ has e2e && step e2e_probe 900 python tools/e2e_probe.py
 has probe && step line_probe 300 python tools/line_probe.py
 has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
 has ablateb && step ablate_bwd 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --bwd
+has ablatec && step ablate_conv 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --convc1
 has ablatek && step ablate_kitti 600 python tools/ablate.py --config kitti --build-modes 0,2,1,3 --lookup-variants 0,1,3
 has configs && step bench_realtime 300 python bench.py --config realtime --no-cpu-baseline --steps 50 --warmup 5 && step bench_realtime_graph 300 python bench.py --config realtime --graph --no-cpu-baseline --steps 200 --warmup 10
 has configs && step bench_middlebury 300 python bench.py --config middlebury --no-cpu-baseline --steps 5 --warmup 2
