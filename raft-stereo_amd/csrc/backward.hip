@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(LookupBwdArgs a) {
 // within the division's error bound, kept for exactness) applies those direct
 // updates first and reloads its chunks, in lookup_bwd_kernel's order, so the
 // results are bit-identical to it.
-template <int R, int NL, int WPE = 1, int PF = 8, bool GVL = false>
+template <int R, int NL, int WPE = 1, int PF = 8, bool GVL = false, bool NTG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_bwd_pre_kernel(LookupBwdArgs a) {
     constexpr int T = 2 * R + 1, NW = 2 * R + 4, NV = (NW + 6) / 4;
     const long long pblk = (long long)blockIdx.x * 256;
@@ -154,7 +154,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     auto issue = [&](int i) {
         if constexpr (!GVL) {
 #pragma unroll
-            for (int t = 0; t < T; ++t) gv[i][t] = go[(long long)(i * T + t) * a.HW];
+            for (int t = 0; t < T; ++t)
+                gv[i][t] = NTG ? __builtin_nontemporal_load(go + (long long)(i * T + t) * a.HW)
+                               : go[(long long)(i * T + t) * a.HW];
         }
         const int W = a.W[i];
         const float xl = x / (float)(1 << i);
@@ -490,9 +492,11 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
     // dev-only A/B: RAFTCORR_LOOKUP_BWD_VARIANT=1 forces the per-level-wait kernel
     int variant = 0;
     if (const char *e = getenv("RAFTCORR_LOOKUP_BWD_VARIANT")) variant = atoi(e);
-    if (variant >= 3 && variant <= 6 && radius == 4 && a.levels == 4) {
+    if (variant >= 3 && variant <= 7 && radius == 4 && a.levels == 4) {
+        // 7: non-temporal output-gradient loads (read once)
         // 6: chunks up front, output gradients loaded per level
         if (variant == 6) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 8, true>), dim3(nblk), dim3(256), 0, s, a);
+        if (variant == 7) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 8, false, true>), dim3(nblk), dim3(256), 0, s, a);
         // 3: occupancy cap 3 waves/SIMD; 4 / 5: one / two levels prefetched ahead
         if (variant == 3) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
         if (variant == 4) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 1>), dim3(nblk), dim3(256), 0, s, a);

@@ -43,8 +43,8 @@ def main():
                     help="time rc_corr_lookup_chain vs the per-level rc_corr_lookup")
     ap.add_argument("--bwd", action="store_true",
                     help="time the backward kernels")
-    ap.add_argument("--bwd-variants", default="0,1,4,6",
-                    help="RAFTCORR_LOOKUP_BWD_VARIANT values (0 product, 1 per-level waits, 3 capped occupancy, 4/5 prefetch 1/2 levels ahead, 6 grad_out loaded per level)")
+    ap.add_argument("--bwd-variants", default="0,1,7",
+                    help="RAFTCORR_LOOKUP_BWD_VARIANT values (0 product, 1 per-level waits, 3 capped occupancy, 4/5 prefetch 1/2 levels ahead, 6 grad_out loaded per level, 7 non-temporal grad_out loads)")
     ap.add_argument("--convc1", action="store_true",
                     help="also time lookup+convc1+relu fused vs separate (MIOpen 1x1 conv)")
     a = ap.parse_args()
