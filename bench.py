@@ -42,9 +42,9 @@ CONFIGS = {
     "sceneflow": (8, 256, 135, 240, 240, 4, 4, 32,
                   "corr path: CorrBlock1D build + 32 lookups, 540x960 -> 135x240 fmaps, "
                   "batch 8/GPU, fp32, 4 levels, radius 4"),
-    "kitti": (8, 256, 94, 311, 311, 4, 4, 32,
-              "corr path: build + 32 lookups, 375x1242 -> 94x311 fmaps, batch 8/GPU "
-              "(64 global at 8 GPUs), bf16 fmaps, bf16 MFMA volume + bf16 pyramid"),
+    "kitti": (64, 256, 94, 311, 311, 4, 4, 32,
+              "corr path: build + 32 lookups, 375x1242 -> 94x311 fmaps, global batch 64 "
+              "split over the GPUs, bf16 fmaps, bf16 MFMA volume + bf16 pyramid"),
     "realtime": (1, 256, 120, 160, 160, 3, 4, 7,
                  "corr path: build + 7 lookups, 480x640 -> 120x160, batch 1, 3 levels"),
     "middlebury": (1, 256, 496, 720, 720, 4, 4, 32,
@@ -71,6 +71,9 @@ def volume_bytes(B, D, H, W1, W2, nbuf, s_in=4, s_pyr=4):
 
 BF16_CONFIGS = {"kitti"}
 ROW_SHARD_CONFIGS = {"middlebury"}
+# BASELINE configs[2]: "batch 64 ... batch-sharded across 2/4/8 GPUs" -- the
+# config's B is the GLOBAL batch, split over the ranks (strong scaling)
+GLOBAL_BATCH_CONFIGS = {"kitti"}
 
 
 def make_inputs(cfg, device, seed, dtype=torch.float32):
@@ -88,31 +91,64 @@ def make_inputs(cfg, device, seed, dtype=torch.float32):
     return f1, f2, coords
 
 
-def cpu_baseline(cfg, seconds_target=15.0):
-    """Time the oracle's ATen-sequence restatement of model.py:267-326
-    (oracle/torch_ref.py) on this host: one pair (B=1) of the same workload."""
+def host_cores():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU
+    quota when one is set (the GPU box shows the whole machine in the mask
+    but gives one GPU's share of it)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def _median_time(fn, reps, budget_s):
+    """Median wall time of ``fn`` over up to ``reps`` runs after one warm-up
+    (fewer when the budget runs out; always at least one timed run)."""
+    fn()
+    times, t_end = [], time.perf_counter() + budget_s
+    while not times or (len(times) < reps and time.perf_counter() < t_end):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    return times[len(times) // 2], len(times)
+
+
+def cpu_baseline(cfg, seconds_target=15.0, full=True):
+    """BASELINE.md §3 on this host's cores, through the oracle's restatement
+    of the reference (oracle/torch_ref.py: model.py:267-326 op for op,
+    including the torch.unique assert at :272; pinned bit-exact to goldens
+    from the reference itself):
+      value     corr path pairs/s: one pair (B=1) of the bench workload,
+                build + ``iters`` lookups;
+      e2e_config1  BASELINE configs[0]: the whole network (network.RAFTStereo
+                with the oracle corr block, pinned to the reference's config-1
+                golden by tests/test_network_cpu.py) on one 1x3x320x720 pair,
+                12 iterations;
+      build / lookup  the corr build alone (GFLOP/s) and one lookup alone
+                (algorithmic GB/s) at the full config-2 shape (B=8).
+    Each is the median of up to 5 runs after one warm-up."""
     from oracle import torch_ref
     B, D, H, W1, W2, L, r, iters, _ = cfg
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    cores, aff, quota = host_cores()
     torch.set_num_threads(cores)
+    budget = seconds_target / 4
     f1, f2, coords = make_inputs((1,) + cfg[1:], "cpu", seed=7)
-    blk = torch_ref.TorchCorrBlock1D(f1, f2, L, r)   # warm-up (allocator, threads)
-    blk(coords[0])
-    times = []
-    t_end = time.perf_counter() + seconds_target
-    reps = 0
-    while reps < 1 or (time.perf_counter() < t_end and reps < 5):
-        t0 = time.perf_counter()
+
+    def corr_pair():
         blk = torch_ref.TorchCorrBlock1D(f1, f2, L, r)
         for it in range(iters):
             blk(coords[it])
-        times.append(time.perf_counter() - t0)
-        reps += 1
-    t = sorted(times)[len(times) // 2]
+    t_pair, n_pair = _median_time(corr_pair, 5, budget)
     cpu_name = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -122,17 +158,49 @@ def cpu_baseline(cfg, seconds_target=15.0):
                     break
     except OSError:
         pass
-    return {"value": 1.0 / t, "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": f"1 pair (B=1) of the same workload, build + {iters} lookups via "
-                      f"oracle/torch_ref.py (reference ATen op sequence incl. the torch.unique "
-                      f"assert), median of {len(times)} after 1 warm-up, {cpu_name}",
-            "sec_per_pair": t}
+    out = {"value": 1.0 / t_pair, "unit": "pairs/s", "cores": cores, "kind": "port",
+           "sample": f"corr path, 1 pair (B=1) of the bench workload: build + {iters} lookups "
+                     f"via oracle/torch_ref.py (the reference's ATen op sequence incl. the "
+                     f"torch.unique assert), median of {n_pair} after 1 warm-up; {cpu_name}",
+           "sec_per_pair": t_pair, "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+    if not full:
+        return out
+
+    # BASELINE configs[0]: one 1x3x320x720 pair, 12 iterations, fp32 CPU
+    from raft_stereo_amd.network import RAFTStereo, StereoArgs
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs(), corr_block=torch_ref.TorchCorrBlock1D).eval()
+    g = torch.Generator().manual_seed(1234)
+    img1 = torch.rand(1, 3, 320, 720, generator=g) * 255
+    img2 = torch.roll(img1, shifts=-8, dims=-1)
+    with torch.no_grad():
+        t_e2e, n_e2e = _median_time(lambda: model(img1, img2, iters=12), 5, seconds_target)
+
+    # build and one lookup alone at the full config shape (B as configured)
+    F1, F2, C = make_inputs(cfg, "cpu", seed=8)
+    t_build, n_build = _median_time(lambda: torch_ref.TorchCorrBlock1D(F1, F2, L, r), 5, budget)
+    blk = torch_ref.TorchCorrBlock1D(F1, F2, L, r)
+    t_look, n_look = _median_time(lambda: blk(C[0]), 5, budget)
+    P = B * H * W1
+    return {**out,
+            "e2e_config1": {"sec_per_pair": t_e2e, "pairs_per_s": 1.0 / t_e2e, "runs": n_e2e,
+                            "workload": "BASELINE configs[0]: network.RAFTStereo (default args, "
+                                        "seeded weights) + oracle corr block, 1x3x320x720, "
+                                        "12 iters, fp32"},
+            "build": {"ms": t_build * 1e3, "runs": n_build,
+                      "gflops": volume_flops(B, D, H, W1, W2) / t_build / 1e9,
+                      "shape": [B, D, H, W1, W2], "levels": L + 1},
+            "lookup": {"ms": t_look * 1e3, "runs": n_look,
+                       "gbs": lookup_bytes(P, L, r) / t_look / 1e9,
+                       "algorithmic_bytes": lookup_bytes(P, L, r)}}
 
 
 def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False,
-                    fuse_step=False):
+                    fuse_step=False, world=1):
     """Whole network (encoders/GRU on PyTorch ops + the HIP corr path) on
-    synthetic pairs at the config's image size: pairs/s and the corr share."""
+    synthetic pairs at the config's image size.  Every rank runs its own batch;
+    the timed region is bracketed by barriers and the MAX over ranks is the
+    job's time, so ``pairs_per_s_all_ranks`` = B * world / max time."""
     from raft_stereo_amd.network import RAFTStereo, StereoArgs
     B, D, H1, W1, W2, L, r, iters, _ = cfg
     torch.manual_seed(0)
@@ -148,14 +216,23 @@ def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False
         for _ in range(warmup):
             model(img1, img2, iters=iters)
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         t0 = time.perf_counter()
         for _ in range(steps):
             model(img1, img2, iters=iters)
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / steps
-    return {"pairs_per_s": B / dt, "ms_per_batch": dt * 1e3, "batch": B, "image": [H, W],
+        if world > 1:
+            dist.barrier()
+        dt = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    return {"pairs_per_s": B / dt, "pairs_per_s_all_ranks": B * world / dt,
+            "ms_per_batch": dt * 1e3, "batch": B, "world": world, "image": [H, W],
             "iters": iters, "mixed_precision": mixed, "fuse_step": fuse_step,
-            "note": "full network; encoders/GRU/heads on PyTorch (MIOpen) ops per north_star"}
+            "note": "full network; encoders/GRU/heads on PyTorch (MIOpen) ops per north_star; "
+                    "max over ranks"}
 
 
 def backward_timing(cfg, f1, f2, coords, reps=3):
@@ -291,6 +368,11 @@ def main():
     torch.cuda.set_device(device)
 
     cfg = CONFIGS[args.config]
+    global_batch = args.config in GLOBAL_BATCH_CONFIGS
+    if global_batch:
+        from raft_stereo_amd.shard import split_range
+        b0, b1 = split_range(cfg[0], rank, world)
+        cfg = (b1 - b0,) + cfg[1:]
     B, D, H, W1, W2, L, r, iters, desc = cfg
     bf16 = args.config in BF16_CONFIGS
     row_shard = args.config in ROW_SHARD_CONFIGS and world > 1
@@ -404,7 +486,10 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     sec = float(elapsed.item())
     ms_per_step = 1e3 * sec / args.steps
-    value = (1 if row_shard else world) * B * args.steps / sec
+    # pairs the whole job processed per step: one row-sharded pair, the global
+    # batch, or B per rank (weak scaling)
+    job_pairs = 1 if row_shard else (CONFIGS[args.config][0] if global_batch else world * B)
+    value = job_pairs * args.steps / sec
 
     vflops = volume_flops(B, D, H, W1, W2)
     s_el = 2 if bf16 else 4
@@ -448,13 +533,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if row_shard else "weak",
+        "scaling": "strong" if (row_shard or global_batch) else "weak",
         "vs_baseline": None,
         "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (randn fmaps, coords_grid - U[0,64) per iteration)",
         "config": {"workload": desc + (" (HIP graph replay)" if args.graph else "")
                    + (f" (rows sharded over {world} ranks)" if row_shard else ""),
-                   "config": args.config, "global_batch": B * (1 if row_shard else world),
+                   "config": args.config, "global_batch": job_pairs,
                    "fmap": [B, D, H, W1], "W2": W2, "levels": L, "radius": r, "iters": iters,
                    "parallelism": (f"row-shard x{world}" if row_shard else f"batch-shard x{world}")},
         "roofline": dominant,
@@ -480,8 +565,7 @@ def main():
             rl["traffic_frac"] = rl["traffic_gbs"] / HBM_PEAK_GBS
         result["upsample"] = upsample_timing(cfg, device)
     if args.e2e_steps > 0 and args.config == "sceneflow":
-        result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1)
-        result["e2e"]["pairs_per_s_all_ranks"] = result["e2e"]["pairs_per_s"] * world
+        result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1, world=world)
         result["e2e"]["corr_path_share"] = (ms_per_step / result["e2e"]["ms_per_batch"])
     if args.e2e_steps > 0 and args.config == "realtime":
         # C5 is latency-bound: whole network per pair, with and without the
@@ -491,7 +575,8 @@ def main():
             "fused_step": e2e_pairs_per_s(cfg, device, max(args.e2e_steps, 10), 3, (480, 640),
                                           fuse_step=True)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds,
+                                              full=args.config == "sceneflow")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

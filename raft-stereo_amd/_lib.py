@@ -9,6 +9,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libraftcorr.so")
+# Same sources built with -DRAFTCORR_DEV: A/B knobs + ablation kernels
+# (tools/ablate.py and the variant bit-identity tests only; never the product).
+DEV_LIB_PATH = os.path.join(_HERE, "_build", "libraftcorr_dev.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 
 RC_F32, RC_BF16 = 0, 1
@@ -40,29 +43,54 @@ SIGNATURES = {
 }
 
 _lib = None
+_dev = None
+_active = None      # set while dev_library() is active
 
 
 class CorrLibError(RuntimeError):
     pass
 
 
+def _open(path):
+    if not os.path.exists(path):
+        raise CorrLibError(
+            f"raft_stereo_amd: HIP library missing at {path}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'`")
+    dll = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(dll, name)
+        fn.restype = res
+        fn.argtypes = args
+    if dll.rc_abi_version() != ABI_VERSION:
+        raise CorrLibError(f"raft_stereo_amd: ABI version mismatch in {path}")
+    return dll
+
+
 def lib():
     """Load (once) and return the CDLL; raise if the HIP library is absent."""
     global _lib
+    if _active is not None:
+        return _active
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise CorrLibError(
-                f"raft_stereo_amd: HIP library missing at {LIB_PATH}; build it with "
-                "`python -c 'import __graft_entry__ as g; g.build()'`")
-        dll = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(dll, name)
-            fn.restype = res
-            fn.argtypes = args
-        if dll.rc_abi_version() != ABI_VERSION:
-            raise CorrLibError("raft_stereo_amd: libraftcorr ABI version mismatch")
-        _lib = dll
+        _lib = _open(LIB_PATH)
     return _lib
+
+
+class dev_library:
+    """``with _lib.dev_library():`` routes every call to libraftcorr_dev.so
+    (the knob-enabled A/B build) for the duration of the block."""
+
+    def __enter__(self):
+        global _dev, _active
+        if _dev is None:
+            _dev = _open(DEV_LIB_PATH)
+        self._prev, _active = _active, _dev
+        return _dev
+
+    def __exit__(self, *exc):
+        global _active
+        _active = self._prev
+        return False
 
 
 def check(rc, what):

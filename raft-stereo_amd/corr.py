@@ -191,11 +191,22 @@ def lookup_convc1(pyramid, coords, num_levels, radius, weight, bias=None, relu=T
     x, cbs = _check_coords(pyramid, coords)
     B, _, H, W1 = coords.shape
     cin = num_levels * (2 * radius + 1)
+    _require_hip(weight, "weight")
+    if weight.device != coords.device:
+        raise RuntimeError("lookup_convc1: weight and coords on different devices")
     w = weight.detach().reshape(weight.shape[0], -1).float().contiguous()
     if w.shape[1] != cin:
         raise RuntimeError(f"lookup_convc1: weight has {w.shape[1]} input channels, lookup gives {cin}")
-    b = bias.detach().float().contiguous() if bias is not None else None
     cout = w.shape[0]
+    b = None
+    if bias is not None:
+        _require_hip(bias, "bias")
+        if bias.device != coords.device:
+            raise RuntimeError("lookup_convc1: bias and coords on different devices")
+        if bias.numel() != cout:
+            raise RuntimeError(f"lookup_convc1: bias has {bias.numel()} elements, weight has {cout} "
+                               "output channels")
+        b = bias.detach().float().contiguous()
     out = torch.empty((B, cout, H, W1), dtype=torch.float32, device=coords.device)
     if B * H * W1 == 0:
         return out
@@ -440,9 +451,16 @@ class CorrBlock1D:
         c1 = coords1.detach().contiguous()
         d = None
         if delta is not None:
+            _require_hip(delta, "delta")
+            if delta.device != c1.device:
+                raise RuntimeError("lookup_step: delta and coords1 on different devices")
             d = delta.detach().float().contiguous()
             if d.shape != c1.shape:
                 raise RuntimeError(f"lookup_step: delta {tuple(d.shape)} != coords {tuple(c1.shape)}")
+        if out is not None:
+            _require_hip(out, "out")
+            if out.device != c1.device:
+                raise RuntimeError("lookup_step: out and coords1 on different devices")
         new = torch.empty_like(c1) if out is None else out
         if new.shape != c1.shape or not new.is_contiguous() or new.dtype != torch.float32:
             raise RuntimeError("lookup_step: out must be a contiguous fp32 (B, 2, H, W1) tensor")

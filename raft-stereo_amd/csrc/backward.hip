@@ -489,9 +489,9 @@ void volume_bwd_kernel(BuildBwdArgs a, int nwg_total) {
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
-    // dev-only A/B: RAFTCORR_LOOKUP_BWD_VARIANT=1 forces the per-level-wait kernel
-    int variant = 0;
-    if (const char *e = getenv("RAFTCORR_LOOKUP_BWD_VARIANT")) variant = atoi(e);
+#ifdef RAFTCORR_DEV
+    // dev library A/B: RAFTCORR_LOOKUP_BWD_VARIANT=1 forces the per-level-wait kernel
+    const int variant = rc::dev_knob("RAFTCORR_LOOKUP_BWD_VARIANT");
     if (variant >= 3 && variant <= 7 && radius == 4 && a.levels == 4) {
         // 7: non-temporal output-gradient loads (read once)
         // 6: chunks up front, output gradients loaded per level
@@ -503,6 +503,9 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
         if (variant == 5) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 2>), dim3(nblk), dim3(256), 0, s, a);
         return hipGetLastError();
     }
+#else
+    const int variant = 0;
+#endif
     if (variant == 0 && radius >= 1 && radius <= 4 && a.levels >= 1 && a.levels <= 4) {
 #define RC_LBWD(RR)                                                                                      \
     switch (a.levels) {                                                                                  \

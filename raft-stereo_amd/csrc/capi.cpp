@@ -85,7 +85,9 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     a.pow2 = is_pow2_float(a.sq) ? 1 : 0;
     a.scale = 1.0f / a.sq;                      // exact when pow2
     a.pyr_bf16 = pyr_dtype == RC_BF16;
-    if (const char *e = getenv("RAFTCORR_STAGGER")) a.stagger = atoi(e);
+#ifdef RAFTCORR_DEV
+    a.stagger = rc::dev_knob("RAFTCORR_STAGGER");
+#endif
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // fp32 fmaps + fp32 pyramid: exact fp32 MFMA.  bf16 fmaps, or a bf16
     // pyramid (bf16-level tolerance requested), take the bf16 MFMA kernel.

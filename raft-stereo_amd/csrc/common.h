@@ -3,7 +3,21 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifdef RAFTCORR_DEV
+#include <stdlib.h>
+#endif
+
 namespace rc {
+
+// Dev-only A/B knobs (environment variables read per launch).  They exist
+// only in libraftcorr_dev.so (built with -DRAFTCORR_DEV, tools/ablate.py);
+// the product library has no knobs, no getenv and no ablation kernels.
+#ifdef RAFTCORR_DEV
+inline int dev_knob(const char *name) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : 0;
+}
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));

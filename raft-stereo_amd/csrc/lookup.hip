@@ -26,8 +26,6 @@
 // whose floor is off by more than one (impossible for |x| < 2^22 by the error
 // bound; kept for safety) takes a guarded scalar path.  Output stores are
 // coalesced along w1.
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "common.h"
@@ -331,6 +329,7 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
 
     // level 0 math + stores while the span is in flight
     finish_level<R, false>(lw0, a, 0, pblk, lrow, [&](int t, float v) {
+        if (!active) return;
         if constexpr (M == 5) __builtin_nontemporal_store(v, outp + (long long)t * a.HW);
         else if (!NOSTORE || v == 1234.5f) outp[(long long)t * a.HW] = v;
     });
@@ -407,12 +406,15 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
                 res[t] = fmaf(w1, v1, w0 * v0);
             }
         }
-        // inactive lanes (tail block) hold pixel P-1's values: storing them
-        // again is a same-value write, so the stores need no predicate
+        // inactive lanes (tail block) stand in for pixel P-1 and store nothing:
+        // with rc_corr_lookup_step in place (coords_out == coords) they may have
+        // read coords the real lane already advanced
+        if (active) {
 #pragma unroll
-        for (int t = 0; t < T; ++t)
-            if constexpr (M == 5) __builtin_nontemporal_store(res[t], outp + (long long)(i * T + t) * a.HW);
-            else if (!NOSTORE || res[t] == 1234.5f) outp[(long long)(i * T + t) * a.HW] = res[t];
+            for (int t = 0; t < T; ++t)
+                if constexpr (M == 5) __builtin_nontemporal_store(res[t], outp + (long long)(i * T + t) * a.HW);
+                else if (!NOSTORE || res[t] == 1234.5f) outp[(long long)(i * T + t) * a.HW] = res[t];
+        }
     };
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
@@ -433,15 +435,16 @@ static hipError_t launch_chain_m(const LookupArgs &a, hipStream_t s, unsigned ld
 
 template <int R>
 static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
-    int variant = 0;
-    if (const char *e = getenv("RAFTCORR_LOOKUP_VARIANT")) variant = atoi(e);
-    if constexpr (R == 4) {   // ablation variants (dev-only), config-2 radius
+#ifdef RAFTCORR_DEV
+    if constexpr (R == 4) {   // ablation variants (dev library), config-2 radius
+        const int variant = dev_knob("RAFTCORR_LOOKUP_VARIANT");
         if (variant == 101) return launch_chain_m<R, 1>(a, s);
         if (variant == 102) return launch_chain_m<R, 2>(a, s);
         if (variant == 103) return launch_chain_m<R, 3>(a, s);
         if (variant == 104) return launch_chain_m<R, 4>(a, s);
         if (variant == 105) return launch_chain_m<R, 5>(a, s);   // non-temporal output stores
     }
+#endif
     return launch_chain_m<R, 0>(a, s);
 }
 
@@ -498,12 +501,12 @@ template <int R>
 static hipError_t launch_conv_r(const LookupArgs &a, int bf16, const float *w, const float *b,
                                 int cout, int relu, float *out, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
-    if (const char *e = getenv("RAFTCORR_CONV_VARIANT")) {   // dev-only A/B: 1 = one level at a time
-        if (atoi(e) == 1 && a.levels == 4 && !bf16) {
-            hipLaunchKernelGGL((lookup_conv_kernel<R, 4, false, false>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
-            return hipGetLastError();
-        }
+#ifdef RAFTCORR_DEV
+    if (dev_knob("RAFTCORR_CONV_VARIANT") == 1 && a.levels == 4 && !bf16) {   // one level at a time
+        hipLaunchKernelGGL((lookup_conv_kernel<R, 4, false, false>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
+        return hipGetLastError();
     }
+#endif
     if (a.levels == 4) {
         if (bf16) hipLaunchKernelGGL((lookup_conv_kernel<R, 4, true>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
         else hipLaunchKernelGGL((lookup_conv_kernel<R, 4, false>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
@@ -536,6 +539,9 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
     // predicated loads.  Variant 1: full windows; 3: levels unrolled (all
     // loads first; ~130 VGPRs).  Measured (tools/ablate.py) before choosing.
     const bool unroll = a.levels == 3 || a.levels == 4;
+#ifndef RAFTCORR_DEV
+    variant = 0;
+#endif
     if (variant == 0 && a.P < kSmallP && unroll) {
         if (a.levels == 4) {
             if (bf16) launch_k<R, 4, true, true, 64>(a, s);
@@ -544,6 +550,7 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
             if (bf16) launch_k<R, 3, true, true, 64>(a, s);
             else launch_k<R, 3, false, true, 64>(a, s);
         }
+#ifdef RAFTCORR_DEV
     } else if (variant == 1) {
         if (bf16) launch_k<R, 0, true, false>(a, s);
         else launch_k<R, 0, false, false>(a, s);
@@ -553,6 +560,7 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
     } else if (variant == 3 && a.levels == 4) {
         if (bf16) launch_k<R, 4, true, true>(a, s);
         else launch_k<R, 4, false, true>(a, s);
+#endif
     } else {
         if (bf16) launch_k<R, 0, true, true>(a, s);
         else launch_k<R, 0, false, true>(a, s);
@@ -562,11 +570,14 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
 
 }  // namespace rc
 
-// RAFTCORR_LOOKUP_VARIANT (dev-only A/B, read per call): see launch_r.
+// RAFTCORR_LOOKUP_VARIANT (dev library only, read per call): see launch_r.
 hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;
-    int variant = 0;
-    if (const char *e = getenv("RAFTCORR_LOOKUP_VARIANT")) variant = atoi(e);
+#ifdef RAFTCORR_DEV
+    const int variant = rc::dev_knob("RAFTCORR_LOOKUP_VARIANT");
+#else
+    const int variant = 0;
+#endif
     switch (radius) {
         case 1: return rc::launch_r<1>(a, pyr_bf16, variant, s);
         case 2: return rc::launch_r<2>(a, pyr_bf16, variant, s);

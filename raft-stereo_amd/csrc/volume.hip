@@ -27,8 +27,6 @@
 // k-steps; one set is loading while the other feeds the MFMAs.  K steps past D
 // load zeros (buffer offset pushed out of range), so there are no per-step
 // guards.
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace rc {
@@ -689,14 +687,15 @@ static void launch_ring(const BuildArgs &a, hipStream_t s) {
 
 template <bool IN_BF16, bool ALIGNED>
 static void launch_bf16(const BuildArgs &a, unsigned nwg, hipStream_t s) {
-    int mode = 0;
-    if (const char *e = getenv("RAFTCORR_BUILD_MODE")) mode = atoi(e);
-    switch (mode) {   // dev-only ablation (see rc_launch_build_f32)
-        case 1: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 1>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
-        case 2: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 2>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
-        case 3: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 3>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
-        default: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 0>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); break;
+#ifdef RAFTCORR_DEV
+    switch (dev_knob("RAFTCORR_BUILD_MODE")) {   // dev-only ablation (see rc_launch_build_f32)
+        case 1: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 1>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); return;
+        case 2: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 2>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); return;
+        case 3: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 3>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); return;
+        default: break;
     }
+#endif
+    hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 0>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
 }
 
 }  // namespace rc
@@ -716,7 +715,7 @@ hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStrea
     return hipGetLastError();
 }
 
-// RAFTCORR_BUILD_MODE (dev-only ablation, read per call): 0 = product (LDS-DMA
+// RAFTCORR_BUILD_MODE (dev library only, read per call): 0 = product (LDS-DMA
 // ring kernel, 3 slots), 2 = ring without epilogue stores, 4 / 5 = 4- / 5-slot
 // ring; 128+flags = the direct-load
 // kernel (flags 1 no operand loads, 2 no stores, 64 stagger).
@@ -725,23 +724,24 @@ hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     const bool vec = (a.W1 % 4 == 0) && (a.W2 % 4 == 0);
-    int mode = 0;
-    if (const char *e = getenv("RAFTCORR_BUILD_MODE")) mode = atoi(e);
     const unsigned n = (unsigned)nwg;
     if (!vec) {
         rc::launch<false, 2, 0>(a, n, s);
-    } else {
-        switch (mode) {
-            case 2: rc::launch_ring<2>(a, s); break;
-            case 4: rc::launch_ring<0, 4>(a, s); break;            // 4-slot ring (dev A/B)
-            case 5: rc::launch_ring<0, 5>(a, s); break;            // 5-slot ring (dev A/B)
-            case 128: rc::launch<true, 2, 0>(a, n, s); break;      // direct-load kernel
-            case 130: rc::launch<true, 2, 2>(a, n, s); break;
-            case 131: rc::launch<true, 2, 3>(a, n, s); break;
-            case 129: rc::launch<true, 2, 1>(a, n, s); break;
-            case 192: rc::launch<true, 2, 64>(a, n, s); break;
-            default: rc::launch_ring<0>(a, s); break;
-        }
+        return hipGetLastError();
     }
+#ifdef RAFTCORR_DEV
+    switch (rc::dev_knob("RAFTCORR_BUILD_MODE")) {
+        case 2: rc::launch_ring<2>(a, s); return hipGetLastError();
+        case 4: rc::launch_ring<0, 4>(a, s); return hipGetLastError();         // 4-slot ring
+        case 5: rc::launch_ring<0, 5>(a, s); return hipGetLastError();         // 5-slot ring
+        case 128: rc::launch<true, 2, 0>(a, n, s); return hipGetLastError();   // direct-load kernel
+        case 130: rc::launch<true, 2, 2>(a, n, s); return hipGetLastError();
+        case 131: rc::launch<true, 2, 3>(a, n, s); return hipGetLastError();
+        case 129: rc::launch<true, 2, 1>(a, n, s); return hipGetLastError();
+        case 192: rc::launch<true, 2, 64>(a, n, s); return hipGetLastError();
+        default: break;
+    }
+#endif
+    rc::launch_ring<0>(a, s);
     return hipGetLastError();
 }

@@ -19,6 +19,13 @@ import torch.distributed as dist
 from .corr import CorrBlock1D
 
 
+def _host_staged(t, group=None):
+    """gloo moves host memory only: CUDA tensors go through host copies when
+    the group is gloo (the CPU tests, and several ranks sharing one GPU in the
+    single-GPU tests).  RCCL ("nccl") takes device tensors directly."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def split_range(n, rank, world):
     """Contiguous [start, stop) of ``n`` items for ``rank``; the first n % world
     ranks take one extra item."""
@@ -38,6 +45,9 @@ def gather_batch(local, world, group=None):
     """all_gather of per-rank batch slices (sizes may differ by one) -> full batch."""
     if world == 1:
         return local
+    dev = local.device
+    if _host_staged(local, group):
+        local = local.cpu()
     n = torch.tensor([local.shape[0]], device=local.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
@@ -48,7 +58,7 @@ def gather_batch(local, world, group=None):
         pad = torch.cat([local, local.new_zeros((cap - local.shape[0],) + tuple(local.shape[1:]))])
     bufs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad.contiguous(), group=group)
-    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0).to(dev)
 
 
 class RowShardedCorr:
@@ -146,6 +156,10 @@ class RowShardedStereo:
             return t
         (r0, r1), (e0, e1) = own, ext
         h = self.halo >> l
+        dev = t.device
+        staged = _host_staged(t, self.group)
+        if staged:
+            t = t.cpu()
         ops, recv = [], []
         prev, nxt = self.rank - 1, self.rank + 1
         if prev >= 0:
@@ -169,7 +183,7 @@ class RowShardedStereo:
             t = t.clone()
             for buf, at in recv:
                 t[:, :, at:at + buf.shape[2]] = buf
-        return t
+        return t.to(dev) if staged else t
 
     # forward ----------------------------------------------------------------
     def forward(self, image1, image2, iters=12):
@@ -235,6 +249,9 @@ class RowShardedStereo:
         """all_gather of per-rank owned-row slabs -> full-height tensor."""
         if self.world == 1:
             return local
+        dev = local.device
+        if _host_staged(local, self.group):
+            local = local.cpu()
         n = torch.tensor([local.shape[2]], device=local.device)
         sizes = [torch.zeros_like(n) for _ in range(self.world)]
         dist.all_gather(sizes, n, group=self.group)
@@ -245,4 +262,4 @@ class RowShardedStereo:
         pad[:, :, :local.shape[2]] = local
         bufs = [torch.empty_like(pad) for _ in range(self.world)]
         dist.all_gather(bufs, pad, group=self.group)
-        return torch.cat([b[:, :, :s] for b, s in zip(bufs, sizes)], dim=2)
+        return torch.cat([b[:, :, :s] for b, s in zip(bufs, sizes)], dim=2).to(dev)

@@ -18,6 +18,11 @@ def convex_upsample(flow, mask, factor):
     fp32.  Inputs of other float dtypes are computed in fp32."""
     _require_hip(flow, "flow")
     _require_hip(mask, "mask")
+    if torch.is_grad_enabled() and (flow.requires_grad or mask.requires_grad):
+        raise RuntimeError("convex_upsample is inference-only (rc_convex_upsample has no "
+                           "backward); call it under torch.no_grad()")
+    if flow.device != mask.device:
+        raise RuntimeError("convex_upsample: flow and mask on different devices")
     if flow.dim() != 4 or mask.dim() != 4:
         raise RuntimeError("convex_upsample: flow and mask must be 4-D")
     N, C, H, W = flow.shape

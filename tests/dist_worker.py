@@ -96,3 +96,55 @@ def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4):
         q.put((rank, traceback.format_exc(), None))
     finally:
         dist.destroy_process_group()
+
+
+def gpu_model():
+    """The default network with the HIP corr block, on cuda:0, seeded weights."""
+    import torch
+    import pkgload
+    pkgload.load()
+    from golden_util import manifest
+    from raft_stereo_amd.network import RAFTStereo, StereoArgs
+    torch.manual_seed(0)
+    case = manifest()["cases"]["e2e_default"]
+    return RAFTStereo(StereoArgs(**case["args"])).eval().to("cuda:0")
+
+
+def rows_images(H=320, W=96):
+    import torch
+    g = torch.Generator().manual_seed(3)
+    img1 = torch.rand(1, 3, H, W, generator=g) * 255
+    return img1, torch.roll(img1, -4, dims=-1)
+
+
+def run_gpu(rank, world, port, q, halo=32, iters=4):
+    """GPU ranks sharing cuda:0 over gloo (host-staged collectives): the
+    batch-sharded network + gather_batch and the row-sharded network + GRU
+    halo exchange, both with the HIP CorrBlock1D (not the oracle)."""
+    import torch
+    import torch.distributed as dist
+    import pkgload
+    pkgload.load()
+    from raft_stereo_amd import CorrBlock1D
+    from raft_stereo_amd.shard import RowShardedStereo, gather_batch, local_batch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = gpu_model()
+        assert net.corr_block is CorrBlock1D
+        img1, img2 = pairs()
+        with torch.no_grad():
+            flows = net(local_batch(img1, rank, world).cuda(), local_batch(img2, rank, world).cuda(),
+                        iters=3)
+            full = gather_batch(flows[-1], world)
+            r1, r2 = rows_images()
+            rs = RowShardedStereo(net, rank, world, halo=halo)
+            preds = rs.forward(r1.cuda(), r2.cuda(), iters=iters)
+            rows = torch.stack([rs.gather_rows(p) for p in preds])
+        q.put((rank, full.cpu(), rows.cpu()))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()

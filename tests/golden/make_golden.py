@@ -168,13 +168,8 @@ def state_hash(model):
     return h.hexdigest()
 
 
-def stereo_pair(B, H, W, seed, shift=6):
-    g = gen(seed)
-    left = torch.rand(B, 3, H, W + shift, generator=g) * 255.0
-    right = left[..., :W].clone()
-    left = left[..., shift:].contiguous()
-    right = (right + torch.randn(B, 3, H, W, generator=g) * 2.0).clamp(0, 255)
-    return left, right
+sys.path.insert(0, os.path.dirname(OUT))
+from golden_util import image_digest, stereo_pair  # noqa: E402  (one generator for both sides)
 
 
 def e2e_case(ref, name, H, W, iters, seed, **kw):
@@ -193,33 +188,61 @@ def e2e_case(ref, name, H, W, iters, seed, **kw):
             "n_params": int(sum(p.numel() for p in model.parameters()))}
 
 
+def e2e_seeded_case(ref, name, H, W, iters, seed, **kw):
+    """A BASELINE-size end-to-end case whose images are NOT stored: the GPU
+    test regenerates them with golden_util.stereo_pair(seed) and checks their
+    sha256 against ``image_sha256``.  Only the final disparity is stored."""
+    args = Args(**kw)
+    torch.manual_seed(0)
+    model = ref.RAFTStereo(args).eval()
+    img1, img2 = stereo_pair(1, H, W, seed)
+    with torch.no_grad():
+        flows = model(img1, img2, iters=iters)
+    disp = flows[-1][:, 0].numpy()                            # (B, H1, W1), final iteration
+    np.savez_compressed(os.path.join(OUT, f"e2e_{name}.npz"), disparity=disp,
+                        iters=np.int32(iters))
+    return {"kind": "e2e_seeded", "H": H, "W": W, "iters": iters, "seed": seed,
+            "args": vars(args), "image_sha256": image_digest(img1, img2),
+            "state_sha256": state_hash(model)}
+
+
 def main():
+    only = sys.argv[1:]          # case names to (re)generate; default: all
     ref, digest = load_reference()
     torch.set_num_threads(8)
     manifest = {"reference_sha256": digest, "torch": torch.__version__,
                 "fixes": [f[1] for f in FIXES], "cases": {}}
-    cases = manifest["cases"]
-    cases["v_w37"] = volume_case(ref, "w37", 2, 16, 3, 37, 37, 4, 1)
-    cases["v_d256"] = volume_case(ref, "d256", 1, 256, 2, 24, 40, 4, 2)
-    cases["v_d128"] = volume_case(ref, "d128", 1, 128, 2, 20, 33, 3, 3)
-    cases["v_w70"] = volume_case(ref, "w70", 1, 64, 1, 70, 70, 4, 4)
-    cases["v_w240"] = volume_case(ref, "w240", 1, 256, 1, 16, 240, 4, 5)
-    cases["l_w37"] = lookup_case(ref, "w37", 2, 16, 3, 37, 37, 4, 4, 11)
-    cases["l_w240"] = lookup_case(ref, "w240", 1, 32, 2, 16, 240, 4, 4, 12)
-    cases["l_w311_r3"] = lookup_case(ref, "w311_r3", 1, 32, 2, 12, 311, 4, 3, 13)
-    cases["l_w720"] = lookup_case(ref, "w720", 1, 16, 2, 8, 720, 4, 4, 14)
-    cases["l_w60_L3"] = lookup_case(ref, "w60_L3", 2, 24, 2, 15, 60, 3, 4, 15)
-    cases["l_special"] = lookup_case(ref, "special", 1, 16, 2, 16, 45, 4, 4, 16, special=True)
-    cases["l_tiny"] = lookup_case(ref, "tiny", 1, 8, 2, 9, 16, 4, 2, 17)
-    cases["b_w37"] = backward_case(ref, "w37", 2, 16, 3, 37, 37, 4, 4, 3, 31)
-    cases["b_w64_L3"] = backward_case(ref, "w64_L3", 1, 32, 2, 40, 64, 3, 3, 2, 32)
-    cases["b_d256"] = backward_case(ref, "d256", 1, 256, 2, 24, 40, 4, 4, 2, 33)
-    cases["b_w45_L2"] = backward_case(ref, "w45_L2", 1, 8, 2, 16, 45, 2, 2, 3, 34)
-    cases["e2e_default"] = e2e_case(ref, "default", 64, 96, 12, 21)
-    cases["e2e_sfgru"] = e2e_case(ref, "sfgru", 64, 80, 6, 22, slow_fast_gru=True, corr_levels=3,
-                                  corr_radius=3)
-    cases["e2e_gru2_ds3"] = e2e_case(ref, "gru2_ds3", 96, 128, 5, 23, n_gru_layers=2, n_downsample=3,
-                                     hidden_dims=[96, 96, 96])
+    if only:
+        with open(os.path.join(OUT, "manifest.json")) as fh:
+            manifest["cases"] = json.load(fh)["cases"]
+    todo = {
+        "v_w37": lambda: volume_case(ref, "w37", 2, 16, 3, 37, 37, 4, 1),
+        "v_d256": lambda: volume_case(ref, "d256", 1, 256, 2, 24, 40, 4, 2),
+        "v_d128": lambda: volume_case(ref, "d128", 1, 128, 2, 20, 33, 3, 3),
+        "v_w70": lambda: volume_case(ref, "w70", 1, 64, 1, 70, 70, 4, 4),
+        "v_w240": lambda: volume_case(ref, "w240", 1, 256, 1, 16, 240, 4, 5),
+        "l_w37": lambda: lookup_case(ref, "w37", 2, 16, 3, 37, 37, 4, 4, 11),
+        "l_w240": lambda: lookup_case(ref, "w240", 1, 32, 2, 16, 240, 4, 4, 12),
+        "l_w311_r3": lambda: lookup_case(ref, "w311_r3", 1, 32, 2, 12, 311, 4, 3, 13),
+        "l_w720": lambda: lookup_case(ref, "w720", 1, 16, 2, 8, 720, 4, 4, 14),
+        "l_w60_L3": lambda: lookup_case(ref, "w60_L3", 2, 24, 2, 15, 60, 3, 4, 15),
+        "l_special": lambda: lookup_case(ref, "special", 1, 16, 2, 16, 45, 4, 4, 16, special=True),
+        "l_tiny": lambda: lookup_case(ref, "tiny", 1, 8, 2, 9, 16, 4, 2, 17),
+        "b_w37": lambda: backward_case(ref, "w37", 2, 16, 3, 37, 37, 4, 4, 3, 31),
+        "b_w64_L3": lambda: backward_case(ref, "w64_L3", 1, 32, 2, 40, 64, 3, 3, 2, 32),
+        "b_d256": lambda: backward_case(ref, "d256", 1, 256, 2, 24, 40, 4, 4, 2, 33),
+        "b_w45_L2": lambda: backward_case(ref, "w45_L2", 1, 8, 2, 16, 45, 2, 2, 3, 34),
+        "e2e_default": lambda: e2e_case(ref, "default", 64, 96, 12, 21),
+        "e2e_sfgru": lambda: e2e_case(ref, "sfgru", 64, 80, 6, 22, slow_fast_gru=True,
+                                      corr_levels=3, corr_radius=3),
+        "e2e_gru2_ds3": lambda: e2e_case(ref, "gru2_ds3", 96, 128, 5, 23, n_gru_layers=2,
+                                         n_downsample=3, hidden_dims=[96, 96, 96]),
+        # BASELINE.json configs[0]: one 1x3x320x720 pair, 12 iterations, default args
+        "e2e_config1": lambda: e2e_seeded_case(ref, "config1", 320, 720, 12, 101),
+    }
+    for name, make in todo.items():
+        if not only or name in only:
+            manifest["cases"][name] = make()
     with open(os.path.join(OUT, "manifest.json"), "w") as fh:
         json.dump(manifest, fh, indent=1)
     print(json.dumps(manifest, indent=1))

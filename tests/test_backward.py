@@ -9,6 +9,8 @@ Tolerances (fp32, the SURVEY §8d contract): max|d|/max|ref| <= 1e-4 and
 rel-L2 <= 1e-5 for the fmap gradients; level gradients <= 1e-5 normalised
 (the only difference is the summation order of tap / call contributions).
 """
+import contextlib
+
 import numpy as np
 import pytest
 import torch
@@ -122,13 +124,16 @@ def test_lookup_backward_prefetch_kernel_bit_identical(L, r, W2, monkeypatch):
         x[0, 0, 0, :6] = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e30, -1e30, 1e-40])
         cs.append(torch.cat([x, torch.randn(B, 1, H, W1, generator=g)], 1).to(DEV))
         gs.append(torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(DEV))
+    from raft_stereo_amd import _lib
     out = {}
     for v in ("1", "0"):
+        # "1": the dev library's knob; "0": the product library
         monkeypatch.setenv("RAFTCORR_LOOKUP_BWD_VARIANT", v)
-        grads = rcorr.grad_buffers(B * H * W1, widths, torch.device(DEV))
-        for c, go in zip(cs, gs):
-            rcorr.lookup_backward(grads, c, go, L, r)
-        torch.cuda.synchronize()
+        with (_lib.dev_library() if v == "1" else contextlib.nullcontext()):
+            grads = rcorr.grad_buffers(B * H * W1, widths, torch.device(DEV))
+            for c, go in zip(cs, gs):
+                rcorr.lookup_backward(grads, c, go, L, r)
+            torch.cuda.synchronize()
         out[v] = grads
     for i in range(L):
         a0 = torch.as_strided(out["0"][i], (out["0"][i].shape[0], out["0"][i].stride(0)),

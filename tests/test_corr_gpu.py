@@ -14,6 +14,7 @@ import torch
 from golden_util import files, load, norm_err, rel_l2, same
 from oracle import coracle
 from raft_stereo_amd import CorrBlock1D
+from raft_stereo_amd import _lib
 from raft_stereo_amd import corr as rcorr
 
 pytestmark = pytest.mark.gpu
@@ -391,7 +392,8 @@ def test_lookup_convc1_prefetch_bit_identical(monkeypatch):
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
         a = blk.lookup_convc1(coords, conv.weight, conv.bias)
         monkeypatch.setenv("RAFTCORR_CONV_VARIANT", "1")
-        b = blk.lookup_convc1(coords, conv.weight, conv.bias)
+        with _lib.dev_library():
+            b = blk.lookup_convc1(coords, conv.weight, conv.bias)
     assert torch.equal(a.nan_to_num(nan=7.0), b.nan_to_num(nan=7.0))
 
 

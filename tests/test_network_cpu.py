@@ -49,3 +49,27 @@ def test_forward_matches_reference_on_cpu(name):
     disp = np.stack([f[:, 0].numpy() for f in flows], 0)
     assert disp.shape == z["disparity"].shape
     assert np.abs(disp - z["disparity"]).max() <= 1e-5
+
+
+SEEDED = {k: v for k, v in manifest()["cases"].items() if v["kind"] == "e2e_seeded"}
+
+
+@pytest.mark.parametrize("name", sorted(SEEDED))
+def test_config1_cpu_counterpart_matches_reference(name):
+    """BASELINE configs[0] (1x3x320x720, 12 iters): the images are regenerated
+    from the golden's seed (sha256 checked) and the CPU counterpart -- this
+    network with the oracle's ATen-sequence corr block, the thing bench.py
+    times as the CPU baseline -- reproduces the reference's final disparity."""
+    from golden_util import image_digest, stereo_pair
+    case = SEEDED[name]
+    z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
+    img1, img2 = stereo_pair(1, case["H"], case["W"], case["seed"])
+    assert image_digest(img1, img2) == case["image_sha256"]
+    model = build(case)
+    assert state_hash(model) == case["state_sha256"]
+    torch.set_num_threads(8)
+    with torch.no_grad():
+        flows = model(img1, img2, iters=case["iters"])
+    disp = flows[-1][:, 0].numpy()
+    assert disp.shape == z["disparity"].shape
+    assert np.abs(disp - z["disparity"]).max() <= 1e-5

@@ -89,3 +89,32 @@ def test_disparity_with_fused_step(name):
     disp = outs[2][:, :, 0].numpy()
     mae = np.abs(disp - z["disparity"]).mean(axis=(1, 2, 3))
     assert (mae <= MAE_PX).all(), f"per-iteration MAE {mae}"
+
+
+SEEDED = {k: v for k, v in manifest()["cases"].items() if v["kind"] == "e2e_seeded"}
+
+
+@pytest.mark.parametrize("fuse", ["none", "step", "convc1"])
+@pytest.mark.parametrize("name", sorted(SEEDED))
+def test_config1_disparity_matches_reference(name, fuse):
+    """BASELINE configs[0]: one 1x3x320x720 pair, 12 iterations, default args,
+    seeded weights (hash checked) -- the HIP corr path inside the network vs
+    the reference's final disparity (model.py:354-383 + the D8 tail), MAE bar
+    0.01 px.  Images are regenerated from the seed and their sha256 checked."""
+    from golden_util import image_digest, stereo_pair
+    case = SEEDED[name]
+    z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
+    img1, img2 = stereo_pair(1, case["H"], case["W"], case["seed"])
+    assert image_digest(img1, img2) == case["image_sha256"]
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs(**case["args"]), fuse_step=fuse == "step",
+                       fuse_convc1=fuse == "convc1").eval()
+    assert model.corr_block is CorrBlock1D
+    model = model.cuda()
+    with torch.no_grad():
+        flows = model(img1.cuda(), img2.cuda(), iters=case["iters"])
+    disp = flows[-1][:, 0].cpu().numpy()
+    assert disp.shape == z["disparity"].shape
+    mae = float(np.abs(disp - z["disparity"]).mean())
+    print(f"{name} [{fuse}]: final MAE {mae:.2e} px, max {np.abs(disp - z['disparity']).max():.2e}")
+    assert mae <= MAE_PX, mae

@@ -1,0 +1,63 @@
+"""The multi-GPU partitioning code on the HIP path.
+
+Batch sharding (configs 2/3) and row sharding with the per-iteration GRU
+halo exchange (config 4) run here with the HIP ``CorrBlock1D`` -- not the
+oracle's CPU block the gloo CPU tests use -- and are compared with the
+unsharded network on the same GPU:
+
+  * world 1 in-process (``gather_batch`` / ``RowShardedStereo`` degenerate to
+    the unsharded code path: same slab arithmetic, no exchange);
+  * world 2: two ranks sharing cuda:0 over gloo (collectives host-staged,
+    shard._host_staged); on an 8-GPU node the same code runs one rank per GPU
+    over RCCL.
+
+Bar: the north_star disparity bar, MAE <= 0.01 px, against the unsharded
+network (the encoder/GRU convs on MIOpen need not be bitwise reproducible
+across batch sizes and slab shapes).
+"""
+import pytest
+import torch
+
+import dist_worker
+from test_shard_dist import _spawn
+
+pytestmark = pytest.mark.gpu
+MAE_PX = 0.01
+
+
+def _reference():
+    net = dist_worker.gpu_model()
+    img1, img2 = dist_worker.pairs()
+    r1, r2 = dist_worker.rows_images()
+    with torch.no_grad():
+        batch = net(img1.cuda(), img2.cuda(), iters=3)[-1].cpu()
+        rows = torch.stack(net(r1.cuda(), r2.cuda(), iters=4)).cpu()
+    return net, batch, rows
+
+
+def test_world1_sharding_on_hip_path():
+    from raft_stereo_amd.shard import RowShardedStereo, gather_batch
+    net, batch, rows = _reference()
+    img1, img2 = dist_worker.pairs()
+    r1, r2 = dist_worker.rows_images()
+    with torch.no_grad():
+        got = gather_batch(net(img1.cuda(), img2.cuda(), iters=3)[-1], 1).cpu()
+        rs = RowShardedStereo(net, 0, 1, halo=32)
+        got_rows = torch.stack([rs.gather_rows(p) for p in rs.forward(r1.cuda(), r2.cuda(), iters=4)])
+    assert (got - batch).abs().mean() <= MAE_PX
+    assert got_rows.shape == rows.shape
+    assert (got_rows.cpu() - rows).abs().mean() <= MAE_PX
+
+
+def test_world2_sharding_on_hip_path():
+    _, batch, rows = _reference()
+    res = _spawn(dist_worker.run_gpu, 2)
+    for r in range(2):
+        full, got_rows = res[r]
+        assert full.shape == batch.shape
+        assert (full - batch).abs().mean() <= MAE_PX, (full - batch).abs().mean()
+        assert got_rows.shape == rows.shape
+        err = (got_rows - rows).abs()
+        print(f"rank {r}: batch MAE {(full - batch).abs().mean():.2e}, rows MAE {err.mean():.2e} "
+              f"max {err.max():.2e}")
+        assert err.mean() <= MAE_PX, err.mean()

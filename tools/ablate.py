@@ -2,8 +2,9 @@
 
     python tools/ablate.py [--config sceneflow] [--rounds 7]
 
-Variants are dev-only env knobs read per launch by libraftcorr:
-RAFTCORR_BUILD_MODE (volume.hip) and RAFTCORR_LOOKUP_VARIANT (lookup.hip).
+Variants are dev-only env knobs read per launch by libraftcorr_dev.so (the
+-DRAFTCORR_DEV build; the product library has none): RAFTCORR_BUILD_MODE
+(volume.hip) and RAFTCORR_LOOKUP_VARIANT (lookup.hip).
 Prints median / min microseconds per launch for each variant.
 """
 import argparse
@@ -18,7 +19,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from raft_stereo_amd import CorrBlock1D  # noqa: E402
+from raft_stereo_amd import _lib  # noqa: E402
 from raft_stereo_amd import corr as rcorr  # noqa: E402
+
+_lib.dev_library().__enter__()   # every call of this tool goes to the knob-enabled build
 
 
 def time_launches(fn, n):

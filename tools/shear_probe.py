@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
-    lib = _lib.lib()
+    lib = _lib.dev_library().__enter__()   # the prototype lives in the dev build only
     fn = lib.rc_dev_lookup_sheared
     fn.restype = ctypes.c_int
     vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
