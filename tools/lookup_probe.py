@@ -1,0 +1,93 @@
+"""How the lookup's time depends on WHERE its coordinates point (dev probe).
+
+    python tools/lookup_probe.py [--config sceneflow] [--reps 5]
+
+The chain lookup (product) and the per-level lookup are event-timed per
+launch, 32 launches back to back like the bench, under coordinate
+distributions that differ only in locality:
+  bench   coords_grid - U[0,64) per pixel, a fresh draw per launch (bench.py);
+  same    one bench draw reused by all 32 launches (upper bound on re-use);
+  row     x ~ U[0, W) anywhere in the row, fresh per launch: the working set
+          is the whole pyramid, so the Infinity Cache cannot help;
+  smooth  a smooth disparity field (neighbouring pixels similar), fresh phase
+          per launch.
+Prints median microseconds per launch and algorithmic GB/s for each.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from raft_stereo_amd import CorrBlock1D, coords_grid  # noqa: E402
+from raft_stereo_amd import corr as rcorr  # noqa: E402
+
+
+def coords_sets(B, H, W1, W2, n, kind, dev):
+    grid = coords_grid(B, H, W1)
+    out = []
+    for it in range(n):
+        g = torch.Generator().manual_seed(1000 + it)
+        c = grid.clone()
+        if kind == "bench" or kind == "same":
+            c[:, 0] -= torch.rand(B, H, W1, generator=g) * 64.0
+        elif kind == "row":
+            c[:, 0] = torch.rand(B, H, W1, generator=g) * (W2 - 1)
+        elif kind == "smooth":
+            ph = float(torch.rand(1, generator=g)) * 6.28
+            w = torch.arange(W1).float().view(1, 1, W1)
+            h = torch.arange(H).float().view(1, H, 1)
+            d = 32 + 24 * torch.sin(w / 17.0 + ph) * torch.cos(h / 13.0 + ph)
+            c[:, 0] -= d + 0.37
+        out.append(c.to(dev))
+        if kind == "same":
+            out = out * n
+            break
+    return out
+
+
+def time_seq(fn, coords, reps):
+    ts = []
+    for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(coords) + 1)]
+        torch.cuda._sleep(3_000_000)
+        ev[0].record()
+        for k, c in enumerate(coords):
+            fn(c)
+            ev[k + 1].record()
+        torch.cuda.synchronize()
+        ts += [ev[k].elapsed_time(ev[k + 1]) * 1e3 for k in range(len(coords))]
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="sceneflow")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
+    dev = torch.device("cuda", 0)
+    f1, f2, _ = bench.make_inputs(bench.CONFIGS[a.config], dev, seed=1)
+    P = B * H * W1
+    lbytes = bench.lookup_bytes(P, L, r)
+    res = {"config": a.config, "P": P, "alg_bytes": lbytes}
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        pyr = blk.corr_pyramid
+        for kind in ("bench", "same", "row", "smooth"):
+            cs = coords_sets(B, H, W1, W2, iters, kind, dev)
+            for name, fn in (("chain", blk), ("per_level", lambda c: rcorr.lookup(pyr, c, L, r))):
+                us = time_seq(fn, cs, a.reps)
+                res[f"{kind}/{name}"] = {"us": round(us, 2),
+                                         "alg_GBps": round(lbytes / (us * 1e-6) / 1e9, 1)}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
