@@ -62,11 +62,11 @@ def volume_flops(B, D, H, W1, W2):
     return 2.0 * B * H * W1 * W2 * D
 
 
-def volume_bytes(B, D, H, W1, W2, nbuf, s_in=4, s_pyr=4):
-    """fmaps read + the ``nbuf`` pyramid levels the build writes (all L+1, or
-    levels 0-1 when the chain lookup recomputes the rest)."""
+def volume_bytes(B, D, H, W1, W2, levels, s_in=4, s_pyr=4):
+    """fmaps read + the pyramid levels the build writes (all L+1, or e.g.
+    levels 0 and 2 when the chain lookup recomputes the rest)."""
     P = B * H * W1
-    return 2 * B * D * H * W1 * s_in + sum(P * (W2 >> l) * s_pyr for l in range(nbuf))
+    return 2 * B * D * H * W1 * s_in + sum(P * (W2 >> l) * s_pyr for l in levels)
 
 
 BF16_CONFIGS = {"kitti"}
@@ -494,8 +494,8 @@ def main():
     vflops = volume_flops(B, D, H, W1, W2)
     s_el = 2 if bf16 else 4
     lbytes = lookup_bytes(P, L, r, s_pyr=s_el)
-    nbuf = sum(t is not None for t in blk._levels)   # levels the build wrote
-    vbytes = volume_bytes(B, D, H, W1, W2, nbuf, s_in=s_el, s_pyr=s_el)
+    written = blk.levels_stored                      # levels the build wrote
+    vbytes = volume_bytes(B, D, H, W1, W2, written, s_in=s_el, s_pyr=s_el)
     traffic = load_traffic(args.traffic).get(args.config, {})
     if bf16:   # HBM-bound in bf16: price the volume in bytes
         vgbs = vbytes / (build_ms * 1e-3) / 1e9
@@ -503,18 +503,21 @@ def main():
                        "frac": vgbs / HBM_PEAK_GBS, "traffic": traffic.get("build_bytes"),
                        "algorithmic_bytes": vbytes, "flops": vflops,
                        "kernel": "rc::build_bf16_kernel", "avg_launch_us": build_ms * 1e3,
-                       "levels_written": nbuf}
+                       "levels_written": written}
     else:
         roof_volume = {"bound": "mfma", "achieved": vflops / (build_ms * 1e-3) / 1e12,
                        "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                        "frac": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
                        "traffic": traffic.get("build_bytes"), "algorithmic_bytes": vbytes,
                        "kernel": "rc::build_f32_ring_kernel<4,0>", "avg_launch_us": build_ms * 1e3,
-                       "levels_written": nbuf}
+                       "levels_written": written}
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
-    lname = (f"rc::lookup_chain_kernel<{r},{L},0>" if blk._chain
+    pair = blk._chain and (L == 2 or (L == 4 and 2 in written))
+    lname = (f"rc::lookup_pair_kernel<{r},{L}>" if pair else
+             f"rc::lookup_chain_kernel<{r},{L},0>" if blk._chain
              else f"rc::lookup_kernel<{r},0,{'true' if bf16 else 'false'},true>")
-    ltraffic = traffic.get("lookup_chain_bytes" if blk._chain else "lookup_bytes")
+    ltraffic = traffic.get("lookup_pair_bytes" if pair else
+                           "lookup_chain_bytes" if blk._chain else "lookup_bytes")
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": lgbs / HBM_PEAK_GBS, "traffic": ltraffic,
                    "algorithmic_bytes": lbytes, "kernel": lname,
@@ -550,8 +553,8 @@ def main():
         "kernel_ms": {"build": build_ms, "lookup_in_loop": lookup_ms,
                       "lookup_per_launch": lookup_launch_ms},
         "cpu_baseline": None,
-        "notes": ("fp32 blocks: the build writes pyramid levels 0-1; every lookup recomputes "
-                  "levels 2..L-1 from level 1 bit-exactly (rc_corr_lookup_chain); levels >= 2 "
+        "notes": (f"fp32 blocks: the build writes pyramid levels {written}; every lookup "
+                  "recomputes the others from them bit-exactly (rc_corr_lookup_chain); the rest "
                   "are materialised only when corr_pyramid is read" if blk._chain else
                   "the build writes all num_levels+1 pyramid levels"),
     }

@@ -13,9 +13,10 @@ so that ``RAFTStereo.forward`` can bind it where the reference does
       (same shape and values, a larger row stride).
   * ``__call__(coords)``  (model.py:297-316)  one lookup launch:
       (B,2,H,W1) fp32 coords -> (B, num_levels*(2r+1), H, W1) fp32.  For an
-      fp32 pyramid with 3-4 levels it is rc_corr_lookup_chain, which reads
-      levels 0-1 only and recomputes the coarser ones (bit-identical to
-      rc_corr_lookup, fewer HBM lines per pixel); otherwise rc_corr_lookup.
+      fp32 pyramid with 2-4 levels it is rc_corr_lookup_chain, which reads two
+      stored levels (0 and 2, or 0 and 1 for 3 levels) and recomputes the
+      others (bit-identical to rc_corr_lookup, fewer HBM lines per pixel);
+      otherwise rc_corr_lookup.
   * ``CorrBlock1D.corr(fmap1, fmap2)``  (model.py:318-326) -> (B,H,W1,1,W2).
   * Autograd: when an fmap requires grad, the lookups
       and the build are autograd nodes.  Each lookup's backward adds its
@@ -113,9 +114,11 @@ def _row_stride(t):
     return t.stride(0) if t.shape[0] > 1 else t.shape[-1]
 
 
-def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True):
+def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, skip=()):
     """Run rc_corr_build: returns ``nbuf`` tensors (B*H*W1, 1, 1, W2 >> l)
-    (row-padded views when ``pad``; values identical either way)."""
+    (row-padded views when ``pad``; values identical either way).  Levels in
+    ``skip`` (>= 1) are computed by the fused epilogue but not stored: their
+    entries are None."""
     B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
     if (W2 >> (nbuf - 1)) < 1:
         raise RuntimeError(
@@ -127,15 +130,16 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True):
     if f1.dtype != f2.dtype:
         f1, f2 = f1.float(), f2.float()
     P = B * H * W1
-    pyr = [_level_buffer(P, W2 >> l, pyramid_dtype, f1.device, pad) for l in range(nbuf)]
+    pyr = [None if l in skip else _level_buffer(P, W2 >> l, pyramid_dtype, f1.device, pad)
+           for l in range(nbuf)]
     if P == 0:
         return pyr
     with torch.cuda.device(f1.device):
         rc = _lib.lib().rc_corr_build(
             f1.data_ptr(), f2.data_ptr(), _dtype_code(f1.dtype), B, D, H, W1, W2,
-            _lib.ptr_array([t.data_ptr() for t in pyr]),
-            _lib.long_array([_row_stride(t) for t in pyr]), nbuf,
-            _dtype_code(pyramid_dtype), _stream(f1.device))
+            _lib.ptr_array([None if t is None else t.data_ptr() for t in pyr]),
+            _lib.long_array([W2 >> l if t is None else _row_stride(t) for l, t in enumerate(pyr)]),
+            nbuf, _dtype_code(pyramid_dtype), _stream(f1.device))
     _lib.check(rc, "rc_corr_build")
     return pyr
 
@@ -236,28 +240,37 @@ def lookup(pyramid, coords, num_levels, radius):
     return out
 
 
+def _chain_args(pyramid, num_levels):
+    """Pointer / width / stride arrays for the pool-chain kernels: the levels
+    present in ``pyramid`` (None = recomputed by the kernel, passed as NULL)."""
+    lv = [None if t is None else
+          (t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous())
+          for t in list(pyramid[:num_levels]) + [None] * (num_levels - len(pyramid))]
+    if any(t is not None and t.dtype != torch.float32 for t in lv):
+        raise TypeError("lookup_chain: fp32 pyramid levels required")
+    W0 = lv[0].shape[-1]
+    ptrs = _lib.ptr_array([None if t is None else t.data_ptr() for t in lv])
+    widths = _lib.int_array([W0 >> i for i in range(num_levels)])
+    lds = _lib.long_array([W0 >> i if t is None else _row_stride(t) for i, t in enumerate(lv)])
+    return lv, ptrs, widths, lds
+
+
 def lookup_chain(pyramid, coords, num_levels, radius):
     """rc_corr_lookup_chain: same result as :func:`lookup` for a pyramid whose
     levels are the avg-pool chain of level 0 (what :func:`build_pyramid`
-    writes).  Only ``pyramid[0]`` and ``pyramid[1]`` are read; later entries
-    may be missing (None) -- the kernel recomputes them (include/raftcorr.h)."""
+    writes).  Entries may be None: with 2 levels, or 4 levels and level 2
+    present, the kernel reads levels 0 and 2 and derives 1 and 3; otherwise it
+    reads levels 0 and 1 and derives the rest (include/raftcorr.h)."""
     x, cbs = _check_coords(pyramid, coords)
     B, _, H, W1 = coords.shape
     out = torch.empty((B, num_levels * (2 * radius + 1), H, W1), dtype=torch.float32,
                       device=coords.device)
     if B * H * W1 == 0:
         return out
-    lv = [t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous()
-          for t in pyramid[:2]]
-    if lv[0].dtype != torch.float32 or lv[1].dtype != torch.float32:
-        raise TypeError("lookup_chain: fp32 pyramid levels required")
-    W0 = lv[0].shape[-1]
-    ptrs = [lv[0].data_ptr()] + [lv[1].data_ptr()] * (num_levels - 1)
-    lds = [_row_stride(lv[0])] + [_row_stride(lv[1])] * (num_levels - 1)
+    keep, ptrs, widths, lds = _chain_args(pyramid, num_levels)
     with torch.cuda.device(coords.device):
         rc = _lib.lib().rc_corr_lookup_chain(
-            _lib.ptr_array(ptrs), _lib.int_array([W0 >> i for i in range(num_levels)]),
-            _lib.long_array(lds), num_levels, radius, x.data_ptr(), cbs, B, H, W1,
+            ptrs, widths, lds, num_levels, radius, x.data_ptr(), cbs, B, H, W1,
             out.data_ptr(), _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup_chain")
     return out
@@ -389,17 +402,24 @@ class CorrBlock1D:
             raise RuntimeError(
                 f"CorrBlock1D: W2={W2} is too narrow for {num_levels} pooling steps: "
                 "avg_pool2d output size is too small (model.py:294)")
-        # fp32 pyramids with 3-4 levels use the chain lookup, which reads levels
-        # 0 and 1 only and recomputes levels 2.. from level 1 bit for bit
-        # (§3.2c of DESIGN.md).  Levels >= 2 are then built only when
-        # ``corr_pyramid`` is read (``lazy_levels``, default on in that case):
-        # same values, same shapes, pooled by the same fp32 ops.
-        self._chain = (pyramid_dtype == torch.float32 and num_levels in (3, 4)
+        # fp32 pyramids with 2-4 levels use a pool-chain lookup that reads two
+        # stored levels and recomputes the others bit for bit (DESIGN.md §3.2c,
+        # §3.2d): 2 or 4 levels -> levels 0 and 2 stored (the pair kernel), 3
+        # levels -> levels 0 and 1 (the level-1 chain kernel).  The other
+        # levels are built only when ``corr_pyramid`` is read (``lazy_levels``,
+        # default on in that case): same values, same shapes, pooled by the
+        # same fp32 ops.
+        self._chain = (pyramid_dtype == torch.float32 and num_levels in (2, 3, 4)
                        and 1 <= radius <= 4)
         lazy = self._chain if lazy_levels is None else (bool(lazy_levels) and self._chain)
         with torch.no_grad():
-            nbuf = 2 if lazy else num_levels + 1
-            self._levels = build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype)
+            if lazy and num_levels == 3:
+                nbuf, skip = 2, ()
+            elif lazy:
+                nbuf, skip = (1, ()) if num_levels == 2 else (3, (1,))
+            else:
+                nbuf, skip = num_levels + 1, ()
+            self._levels = build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype, skip=skip)
             self._levels += [None] * (num_levels + 1 - nbuf)
         self._state = self._token = None
         if grad:
@@ -417,6 +437,11 @@ class CorrBlock1D:
                     if self._levels[l] is None:
                         self._levels[l] = pool_level(self._levels[l - 1])
         return self._levels
+
+    @property
+    def levels_stored(self):
+        """Indices of the pyramid levels currently held in memory."""
+        return [l for l, t in enumerate(self._levels) if t is not None]
 
     @corr_pyramid.setter
     def corr_pyramid(self, levels):
@@ -470,13 +495,8 @@ class CorrBlock1D:
         if B * H * W1 == 0:
             return corr, new, flow
         if self._chain:
-            lv = self._levels[:2]
-            W0 = lv[0].shape[-1]
-            ptrs = _lib.ptr_array([lv[0].data_ptr()] + [lv[1].data_ptr()] * (L - 1))
-            widths = _lib.int_array([W0 >> i for i in range(L)])
-            lds = _lib.long_array([_row_stride(lv[0])] + [_row_stride(lv[1])] * (L - 1))
+            keep, ptrs, widths, lds = _chain_args(self._levels, L)
             dt = _lib.RC_F32
-            keep = lv
         else:
             keep, ptrs, widths, lds, dt = _level_args(self.corr_pyramid, L)
         with torch.cuda.device(c1.device):

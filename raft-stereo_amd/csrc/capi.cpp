@@ -62,7 +62,12 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     if ((long long)B * H * W1 == 0) return RC_OK;
     if (!fmap1 || !fmap2 || !aligned16(fmap1) || !aligned16(fmap2))
         return fail(RC_EINVAL, "rc_corr_build: feature maps must be non-null and 16-byte aligned");
+    const int nfused = nbuf < 7 ? nbuf : 7;
     for (int l = 0; l < nbuf; ++l) {
+        // a NULL level l >= 1 inside the fused epilogue is computed (the next
+        // level needs it) but not stored; later levels are pooled from memory
+        const bool may_skip = l >= 1 && l < nfused && (nbuf <= 7 || l < 6);
+        if (!pyr[l] && may_skip) continue;
         if (!pyr[l] || !aligned16(pyr[l]))
             return fail(RC_EINVAL, "rc_corr_build: pyramid buffer %d null or not 16-byte aligned", l);
         if (pyr_ld && pyr_ld[l] < (long)(W2 >> l))
@@ -74,7 +79,7 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     a.f1 = fmap1;
     a.f2 = fmap2;
     a.B = B; a.D = D; a.H = H; a.W1 = W1; a.W2 = W2;
-    a.nfused = nbuf < 7 ? nbuf : 7;
+    a.nfused = nfused;
     for (int l = 0; l < a.nfused; ++l) {
         a.lvl[l] = pyr[l];
         a.ld[l] = pyr_ld ? pyr_ld[l] : (W2 >> l);
@@ -127,7 +132,7 @@ namespace {
 int prep_lookup(const char *who, const void *const *pyr, const int *widths, const long *pyr_ld,
                 int pyr_dtype, int levels, int radius, const float *coords_x,
                 long coord_batch_stride, int B, int H, int W1, const float *out, rc::LookupArgs &a,
-                bool *empty) {
+                bool *empty, bool allow_null = false) {
     *empty = false;
     if (levels < 1 || levels > RC_MAX_LEVELS)
         return fail(RC_EINVAL, "%s: levels=%d outside 1..%d", who, levels, RC_MAX_LEVELS);
@@ -148,6 +153,12 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
     a = rc::LookupArgs{};
     for (int i = 0; i < levels; ++i) {
         if (widths[i] < 1) return fail(RC_EINVAL, "%s: level %d width %d", who, i, widths[i]);
+        if (!pyr[i] && allow_null && i > 0) {      // recomputed by the kernel, never read
+            a.lvl[i] = nullptr;
+            a.W[i] = widths[i];
+            a.ld[i] = widths[i];
+            continue;
+        }
         if (!pyr[i] || !aligned16(pyr[i]))
             return fail(RC_EINVAL, "%s: level %d null or not 16-byte aligned", who, i);
         a.lvl[i] = pyr[i];
@@ -162,6 +173,40 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
     a.P = P;
     a.HW = H * W1;
     a.levels = levels;
+    return RC_OK;
+}
+}  // namespace
+
+namespace {
+// Which pool-chain kernel serves a request (rc_corr_lookup_chain and the
+// chain mode of rc_corr_lookup_step): the pair kernel (reads levels 0 and 2)
+// for 2 levels, or for 4 levels when level 2 is given; otherwise the level-1
+// chain kernel (reads levels 0 and 1) for 3-4 levels.
+int chain_kind(const char *who, const void *const *pyr, const int *widths, int levels, int radius,
+               bool *pair) {
+    if (levels < 2 || levels > 4 || radius < 1 || radius > 4)
+        return fail(RC_EUNSUPPORTED, "%s: levels 2..4 and radius 1..4 only", who);
+    for (int i = 1; i < levels; ++i)
+        if (widths[i] != widths[i - 1] / 2)
+            return fail(RC_EINVAL, "%s: width %d of level %d is not floor(%d/2)", who, widths[i], i,
+                        widths[i - 1]);
+    *pair = levels == 2 || (levels == 4 && pyr[2] != nullptr);
+    if (!*pair && !pyr[1])
+        return fail(RC_EINVAL, "%s: %d levels need level 1 (or level 2 with 4 levels)", who, levels);
+    if (!*pair && levels < 3)
+        return fail(RC_EUNSUPPORTED, "%s: the level-1 chain needs 3..4 levels", who);
+    return RC_OK;
+}
+
+// Row strides the chain kernels read with 16-B chunks must be multiples of 4.
+int chain_strides(const char *who, const rc::LookupArgs &a, bool pair) {
+    const int need[2] = {0, pair ? 2 : 1};
+    for (int k = 0; k < 2; ++k) {
+        const int i = need[k];
+        if (i < a.levels && a.ld[i] % 4 != 0)
+            return fail(RC_EINVAL, "%s: level-%d row stride %lld is not a multiple of 4", who, i,
+                        a.ld[i]);
+    }
     return RC_OK;
 }
 }  // namespace
@@ -190,20 +235,15 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
     rc::LookupArgs a;
     bool empty;
     int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, RC_F32, levels, radius,
-                         coords_x, coord_batch_stride, B, H, W1, out, a, &empty);
+                         coords_x, coord_batch_stride, B, H, W1, out, a, &empty, true);
     if (rc) return rc;
-    if (levels < 3 || levels > 4 || radius > 4)
-        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: levels 3..4 and radius 1..4 only");
-    for (int i = 1; i < levels; ++i)
-        if (widths[i] != widths[i - 1] / 2)
-            return fail(RC_EINVAL, "rc_corr_lookup_chain: width %d of level %d is not floor(%d/2)",
-                        widths[i], i, widths[i - 1]);
+    bool pair;
+    if ((rc = chain_kind("rc_corr_lookup_chain", pyr, widths, levels, radius, &pair))) return rc;
     if (empty) return RC_OK;
-    if (a.ld[1] % 4 != 0)
-        return fail(RC_EINVAL, "rc_corr_lookup_chain: level-1 row stride %lld is not a multiple of 4",
-                    a.ld[1]);
     a.out = out;
-    return hip_rc(rc_launch_lookup_chain(a, radius, reinterpret_cast<hipStream_t>(stream)),
+    if ((rc = chain_strides("rc_corr_lookup_chain", a, pair))) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    return hip_rc(pair ? rc_launch_lookup_pair(a, radius, s) : rc_launch_lookup_chain(a, radius, s),
                   "rc_corr_lookup_chain: launch");
 }
 
@@ -216,20 +256,16 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
     rc::LookupArgs a;
     bool empty;
     int rc = prep_lookup("rc_corr_lookup_step", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
-                         coords1, 2L * H * W1, B, H, W1, out, a, &empty);
+                         coords1, 2L * H * W1, B, H, W1, out, a, &empty, chain != 0);
     if (rc || empty) return rc;
     if (!coords1_out || !flow_out)
         return fail(RC_EINVAL, "rc_corr_lookup_step: null coords1_out / flow_out");
+    bool pair = false;
     if (chain) {
-        if (pyr_dtype != RC_F32 || levels < 3 || levels > 4 || radius > 4)
-            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: chain needs fp32, levels 3..4, "
-                        "radius 1..4");
-        for (int i = 1; i < levels; ++i)
-            if (widths[i] != widths[i - 1] / 2)
-                return fail(RC_EINVAL, "rc_corr_lookup_step: width %d of level %d is not "
-                            "floor(%d/2)", widths[i], i, widths[i - 1]);
-        if (a.ld[1] % 4 != 0)
-            return fail(RC_EINVAL, "rc_corr_lookup_step: level-1 row stride not a multiple of 4");
+        if (pyr_dtype != RC_F32)
+            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: chain needs an fp32 pyramid");
+        if ((rc = chain_kind("rc_corr_lookup_step", pyr, widths, levels, radius, &pair))) return rc;
+        if ((rc = chain_strides("rc_corr_lookup_step", a, pair))) return rc;
     }
     a.out = out;
     a.step = 1;
@@ -238,7 +274,8 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
     a.coords_out = coords1_out;
     a.flow_out = flow_out;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return hip_rc(chain ? rc_launch_lookup_chain(a, radius, s)
+    return hip_rc(chain ? (pair ? rc_launch_lookup_pair(a, radius, s)
+                                : rc_launch_lookup_chain(a, radius, s))
                         : rc_launch_lookup(a, radius, pyr_dtype == RC_BF16, s),
                   "rc_corr_lookup_step: launch");
 }

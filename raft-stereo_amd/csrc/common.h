@@ -150,6 +150,7 @@ hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, h
 hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf16, const float *w,
                                  const float *b, int cout, int relu, float *out, hipStream_t s);
 hipError_t rc_launch_lookup_chain(const rc::LookupArgs &a, int radius, hipStream_t s);
+hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s);
 hipError_t rc_launch_convex_upsample(const float *flow, const float *mask, int N, int C, int H,

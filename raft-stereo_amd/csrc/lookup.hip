@@ -421,6 +421,204 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
     if constexpr (TOP >= 3) level(std::integral_constant<int, 3>{});
 }
 
+// ---- lookup over a pool-chain pyramid stored as levels 0 and 2 ("pair") ----
+// Level 2k+1 element j is the pairwise mean of level-2k elements 2j, 2j+1
+// (model.py:294, the fp32 ops (a + b) * 0.5), so ONE span of level 2k feeds
+// the windows of both levels 2k and 2k+1:
+//   span  = level-2k elements [2(m-R-1), 2(m+R+3)),  m = floor(x / 2^(2k+1))
+//   level 2k+1, window element jj (element m-R-1+jj) = mean(span[2jj], span[2jj+1])
+//   level 2k,   window element jj (element n-R-1+jj) = span[dd+R+1+jj],
+//               n = floor(x / 2^(2k)) = 2m + dd, dd in {0, 1}
+// With 4 levels the build stores levels 0 and 2 only and a pixel reads two
+// such spans (2(2r+4) elements each): ~2.8 128-B lines per pixel at the bench
+// coordinates against ~3.0 for the level-1 chain (level-0 window + level-1
+// span) and ~4.4 for one window per level, in 14 instead of
+// 16 16-B loads per lane, and with fewer selects.  Window elements outside
+// [0, W_level) are zeroed once per level, which is exactly the reference's
+// per-tap zero padding (a tap reads window elements x0 and x0+1 only).
+template <int R>
+struct PairSpan {
+    static constexpr int NW = 2 * R + 4;              // window elements per level
+    static constexpr int NS = 2 * NW;                 // span elements
+    static constexpr int NC = (NS + 2 + 3) / 4;       // 16-B chunks (start misaligned by 0 or 2)
+    f32x4 q[NC];
+    float m, n;                                       // window centres of the odd / even level
+    int sh;                                           // span start - chunk base: 0 or 2
+    bool inwin, valid;
+};
+
+// Exact element range [f, l] (clipped to [0, W-1]) the taps of one level read.
+template <int R>
+__device__ __forceinline__ void tap_span(float xl, int W, int &f, int &l) {
+    const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+    const DivRN dv = div_prep(Wm1);
+    const float pa = ((div_rn(2.0f * ((float)(-R) + xl), dv) - 1.0f) + 1.0f) * half;
+    const float pb = ((div_rn(2.0f * ((float)R + xl), dv) - 1.0f) + 1.0f) * half;
+    f = max((int)floorf(pa), 0);
+    l = min((int)floorf(pb) + 1, W - 1);
+}
+
+template <int R>
+__device__ __forceinline__ void issue_pair(PairSpan<R> &ps, const LookupArgs &a, int lo, float x,
+                                           long long pblk, long long lrow) {
+    typedef PairSpan<R> PS;
+    const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+    const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+    // false for NaN; outside it every tap of both levels is zero padding
+    ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));
+    ps.m = ps.inwin ? floorf(xhi) : 0.0f;
+    ps.n = ps.inwin ? floorf(xlo) : 0.0f;
+    const int dd = (int)ps.n - 2 * (int)ps.m;
+    ps.valid = ps.inwin && (dd == 0 || dd == 1);      // a subnormal x can break it
+    int lo_e = 0x7FFFFFFF, hi_e = -1;
+    if (ps.inwin) {
+        int f, l;
+        tap_span<R>(xlo, Wlo, f, l);
+        if (f <= l) { lo_e = f; hi_e = l; }
+        tap_span<R>(xhi, Whi, f, l);
+        if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
+    }
+    const int sa = 2 * ((int)ps.m - R - 1);
+    const int ea = sa & ~3;
+    ps.sh = sa - ea;
+    const long long ld = a.ld[lo];
+    const float *lvl = static_cast<const float *>(a.lvl[lo]);
+    const auto rs = make_rsrc(lvl + pblk * ld, clamp_bytes((a.P - pblk) * ld * 4));
+#pragma unroll
+    for (int k = 0; k < PS::NC; ++k) {
+        const int cs = ea + 4 * k;
+        // lo_e >= 0 and hi_e < Wlo: a loaded chunk starts inside the row and
+        // ends inside its 16-B padded extent (ld % 4 == 0)
+        const bool ok = cs <= hi_e && cs + 3 >= lo_e;
+        ps.q[k] = ld4(rs, ok ? (uint32_t)((lrow * ld + cs) * 4) : 0xFFFFFF00u);
+    }
+}
+
+// Taps of one level from its zero-padded window w[NW] (element nwin-R-1+jj):
+// the reference's fp32 sequence (see lookup_kernel); `bad` flags a tap whose
+// floor left the window (unreachable within the division's error bound).
+template <int R>
+__device__ __forceinline__ void window_taps(const float *w, float xl, float nwin, int W, bool chk,
+                                            float *res, bool &bad) {
+    constexpr int T = 2 * R + 1;
+    const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+    const DivRN dv = div_prep(Wm1);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const float xt = (float)(t - R) + xl;
+        const float xn = div_rn(2.0f * xt, dv) - 1.0f;
+        const float xp = (xn + 1.0f) * half;
+        const float x0 = floorf(xp);
+        const float w1 = xp - x0, w0 = 1.0f - w1;
+        const float nt = nwin + (float)(t - R);
+        const bool lo_ = x0 < nt, hi_ = x0 > nt;
+        const float v0 = lo_ ? w[t] : (hi_ ? w[t + 2] : w[t + 1]);
+        const float v1 = lo_ ? w[t + 1] : (hi_ ? w[t + 3] : w[t + 2]);
+        bad |= chk && !(fabsf(x0 - nt) <= 1.0f);
+        res[t] = fmaf(w1, v1, w0 * v0);
+    }
+}
+
+// The (unreachable within the error bound) memory path for one level: every
+// tap re-read, level-i element k = pool of S consecutive span-level elements.
+template <int R, int S>
+__device__ __forceinline__ void level_taps_mem(const float *row, float xl, int W, float *res) {
+    constexpr int T = 2 * R + 1;
+    const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+    const DivRN dv = div_prep(Wm1);
+    for (int t = 0; t < T; ++t) {
+        const float xt = (float)(t - R) + xl;
+        const float xn = div_rn(2.0f * xt, dv) - 1.0f;
+        const float xp = (xn + 1.0f) * half;
+        const float x0 = floorf(xp);
+        const float w1 = xp - x0, w0 = 1.0f - w1;
+        const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+        const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+        const float v0 = ok0 ? derived_elem<S>(row, (long long)x0) : 0.0f;
+        const float v1 = ok1 ? derived_elem<S>(row, (long long)x0 + 1) : 0.0f;
+        res[t] = fmaf(w1, v1, w0 * v0);
+    }
+}
+
+template <int R, class Sink>
+__device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupArgs &a, int lo,
+                                            float x, long long pp, Sink &&sink) {
+    typedef PairSpan<R> PS;
+    constexpr int T = 2 * R + 1, NW = PS::NW, NS = PS::NS;
+    const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+    // span element j = chunk element j + sh, sh in {0, 2}
+    float s[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const float v0 = ps.q[j >> 2][j & 3];
+        const float v2 = ps.q[(j + 2) >> 2][(j + 2) & 3];
+        s[j] = ps.sh ? v2 : v0;
+    }
+    const int mi = (int)ps.m - R - 1, ni = (int)ps.n - R - 1;
+    const int dd = (int)ps.n - 2 * (int)ps.m;
+    float wodd[NW], weven[NW];
+#pragma unroll
+    for (int jj = 0; jj < NW; ++jj) {
+        const float pm = (s[2 * jj] + s[2 * jj + 1]) * 0.5f;      // model.py:294 in fp32
+        wodd[jj] = (unsigned)(mi + jj) < (unsigned)Whi ? pm : 0.0f;
+        const float e = dd == 0 ? s[R + 1 + jj] : s[R + 2 + jj];
+        weven[jj] = (unsigned)(ni + jj) < (unsigned)Wlo ? e : 0.0f;
+    }
+    const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+    float r0[T], r1[T];
+    bool bad = !ps.valid && ps.inwin;
+    window_taps<R>(weven, xlo, ps.n, Wlo, ps.inwin, r0, bad);
+    window_taps<R>(wodd, xhi, ps.m, Whi, ps.inwin, r1, bad);
+    if (__builtin_expect(bad, 0)) {   // one wave-level check for the pair
+        const float *row = static_cast<const float *>(a.lvl[lo]) + pp * a.ld[lo];
+        level_taps_mem<R, 1>(row, xlo, Wlo, r0);
+        level_taps_mem<R, 2>(row, xhi, Whi, r1);
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) sink(lo * T + t, r0[t]);
+#pragma unroll
+    for (int t = 0; t < T; ++t) sink((lo + 1) * T + t, r1[t]);
+}
+
+// NL = 2 (levels 0-1) or 4 (levels 0-3; level 2 stored, levels 1 and 3 derived).
+template <int R, int NL>
+__global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
+    static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
+    const long long pblk = (long long)blockIdx.x * 256;
+    const long long p = pblk + threadIdx.x;
+    const bool active = p < a.P;
+    const long long pp = active ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    const float x = pixel_x(a, bimg, rem, active);
+    float *outp = a.out + bimg * (long long)(NL * (2 * R + 1)) * a.HW + rem;
+    const long long lrow = pp - pblk;
+    auto sink = [&](int ch, float v) {
+        if (active) outp[(long long)ch * a.HW] = v;
+    };
+    PairSpan<R> s0;
+    issue_pair<R>(s0, a, 0, x, pblk, lrow);
+    if constexpr (NL == 4) {
+        PairSpan<R> s2;
+        issue_pair<R>(s2, a, 2, x, pblk, lrow);
+        finish_pair<R>(s0, a, 0, x, pp, sink);
+        finish_pair<R>(s2, a, 2, x, pp, sink);
+    } else {
+        finish_pair<R>(s0, a, 0, x, pp, sink);
+    }
+}
+
+template <int R>
+static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
+    const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    if (a.levels == 4)
+        hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+    else if (a.levels == 2)
+        hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 template <int R, int M>
 static hipError_t launch_chain_m(const LookupArgs &a, hipStream_t s, unsigned lds = 0) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
@@ -587,6 +785,17 @@ hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, h
         case 6: return rc::launch_r<6>(a, pyr_bf16, variant, s);
         case 7: return rc::launch_r<7>(a, pyr_bf16, variant, s);
         case 8: return rc::launch_r<8>(a, pyr_bf16, variant, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, hipStream_t s) {
+    if (a.P <= 0) return hipSuccess;
+    switch (radius) {
+        case 1: return rc::launch_pair_r<1>(a, s);
+        case 2: return rc::launch_pair_r<2>(a, s);
+        case 3: return rc::launch_pair_r<3>(a, s);
+        case 4: return rc::launch_pair_r<4>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

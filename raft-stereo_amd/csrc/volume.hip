@@ -244,7 +244,8 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
         // Levels >= 1 from the wave-private LDS images (in-order LDS within a
         // wave: no barrier needed).  Level l+1 = pairwise mean of level l,
         // read back from LDS in fp32: the same ops as avg_pool2d (:294).
-        store_staged_any<FM>(stA, 1, a.lvl[1], a.ld[1], bf, rowbase, m0, n0, W1, W2 >> 1, lane);
+        // a NULL level is computed (the next one needs it) but not stored
+        if (a.lvl[1]) store_staged_any<FM>(stA, 1, a.lvl[1], a.ld[1], bf, rowbase, m0, n0, W1, W2 >> 1, lane);
         float *src = stA, *dst = stB;
         for (int l = 2; l < a.nfused; ++l) {
             const int cw = 64 >> l, cwp = 2 * cw;
@@ -254,7 +255,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
                 const f32x2 pr = *reinterpret_cast<const f32x2 *>(src + R * cwp + 2 * j);
                 dst[R * cw + j] = (pr[0] + pr[1]) * 0.5f;
             }
-            store_staged_any<FM>(dst, l, a.lvl[l], a.ld[l], bf, rowbase, m0, n0, W1, W2 >> l, lane);
+            if (a.lvl[l]) store_staged_any<FM>(dst, l, a.lvl[l], a.ld[l], bf, rowbase, m0, n0, W1, W2 >> l, lane);
             float *t = src;
             src = dst;
             dst = t;

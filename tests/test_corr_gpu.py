@@ -164,6 +164,9 @@ CHAIN_SHAPES = [
     (1, 16, 2, 60, 61, 3, 4),       # 3 levels: span start at even offsets
     (2, 8, 2, 33, 130, 3, 2),
     (1, 8, 2, 20, 16, 4, 1),        # W2 = 16: level 3 of width 2
+    (1, 16, 2, 50, 50, 2, 4),       # 2 levels: the pair kernel on level 0 alone
+    (2, 8, 2, 33, 61, 2, 2),
+    (1, 8, 3, 70, 77, 4, 2),        # odd level-2 width (19), level 3 of 9
 ]
 
 
@@ -179,10 +182,15 @@ def special_coords(B, H, W1, W2, g):
 
 
 @pytest.mark.parametrize("shape", CHAIN_SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_chain_lookup_bitexact(shape):
-    """rc_corr_lookup_chain (levels >= 2 recomputed from level 1) == the
-    per-level lookup == the oracle, bit for bit, incl. NaN/inf/subnormal x."""
+@pytest.mark.parametrize("stored", ["default", "level1", "level2"])
+def test_chain_lookup_bitexact(shape, stored):
+    """rc_corr_lookup_chain == the per-level lookup == the oracle, bit for bit,
+    incl. NaN/inf/subnormal x, for each pool-chain kernel: the block's default
+    (levels 0+2 stored -> pair kernel for 2/4 levels; 0+1 for 3), levels 0+1
+    only (the level-1 chain kernel) and levels 0+2 only (the pair kernel)."""
     B, D, H, W1, W2, L, r = shape
+    if stored == "level1" and L < 3 or stored == "level2" and L not in (2, 4):
+        pytest.skip("kernel not defined for this level count")
     g = torch.Generator().manual_seed(900 + sum(shape))
     f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
     f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
@@ -190,17 +198,35 @@ def test_chain_lookup_bitexact(shape):
     with torch.no_grad():
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
         assert blk._chain
-        a = rcorr.lookup_chain(blk.corr_pyramid, coords.to(DEV), L, r).cpu().numpy()
+        if stored == "default":
+            a = blk(coords.to(DEV)).cpu().numpy()
+        else:
+            keep = {"level1": (0, 1), "level2": (0, 2)}[stored]
+            lv = [t if i in keep else None for i, t in enumerate(blk.corr_pyramid[:L])]
+            a = rcorr.lookup_chain(lv, coords.to(DEV), L, r).cpu().numpy()
         b = rcorr.lookup(blk.corr_pyramid, coords.to(DEV), L, r).cpu().numpy()
     assert same(a, b)
     assert same(a, coracle.corr_lookup(pyr_np(blk)[:L], coords.numpy(), L, r))
+
+
+def test_chain_block_stores_two_levels():
+    """An fp32 block with 2-4 levels stores the two levels its chain kernel
+    reads (0+2, or 0+1 for 3 levels); the others appear on first read of
+    corr_pyramid."""
+    f = torch.randn(1, 8, 2, 64, device=DEV)
+    with torch.no_grad():
+        assert CorrBlock1D(f, f, num_levels=4).levels_stored == [0, 2]
+        assert CorrBlock1D(f, f, num_levels=3).levels_stored == [0, 1]
+        assert CorrBlock1D(f, f, num_levels=2).levels_stored == [0]
+        blk = CorrBlock1D(f, f, num_levels=4)
+        assert len(blk.corr_pyramid) == 5 and blk.levels_stored == [0, 1, 2, 3, 4]
 
 
 def test_chain_not_used_for_bf16_or_other_levels():
     f = torch.randn(1, 8, 2, 64, device=DEV)
     with torch.no_grad():
         assert not CorrBlock1D(f, f, num_levels=4, pyramid_dtype=torch.bfloat16)._chain
-        assert not CorrBlock1D(f, f, num_levels=2)._chain
+        assert not CorrBlock1D(f, f, num_levels=1)._chain
         assert not CorrBlock1D(f, f, num_levels=5, radius=2)._chain
         assert not CorrBlock1D(f, f, num_levels=4, radius=5)._chain
 
@@ -400,9 +426,10 @@ def test_lookup_convc1_prefetch_bit_identical(monkeypatch):
 @pytest.mark.parametrize("shape", [(2, 64, 3, 240, 240, 4, 4), (1, 32, 2, 311, 311, 3, 3),
                                    (1, 16, 2, 45, 61, 4, 2)], ids=lambda s: "x".join(map(str, s)))
 def test_lazy_levels_equal_fused_epilogue(shape):
-    """Default fp32 blocks write levels 0-1 in the build and pool levels >= 2
-    on first access to corr_pyramid; the eager build writes every level in
-    the fused epilogue.  Same values bit for bit, same lookups."""
+    """Default fp32 blocks write two levels in the build (0+2, or 0+1 for 3
+    levels) and pool the others on first access to corr_pyramid; the eager
+    build writes every level in the fused epilogue.  Same values bit for bit,
+    same lookups."""
     B, D, H, W1, W2, L, r = shape
     g = torch.Generator().manual_seed(1234 + sum(shape))
     f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
@@ -411,9 +438,10 @@ def test_lazy_levels_equal_fused_epilogue(shape):
     with torch.no_grad():
         lazy = CorrBlock1D(f1, f2, num_levels=L, radius=r)
         eager = CorrBlock1D(f1, f2, num_levels=L, radius=r, lazy_levels=False)
-        assert lazy._levels[2] is None and eager._levels[2] is not None
+        stored = lazy.levels_stored
+        assert len(stored) == 2 and eager.levels_stored == list(range(L + 1))
         a, b = lazy(coords), eager(coords)
-        assert lazy._levels[2] is None                 # the lookup did not need them
+        assert lazy.levels_stored == stored            # the lookup did not need the others
     assert same(a.cpu().numpy(), b.cpu().numpy())
     pl, pe = pyr_np(lazy), pyr_np(eager)
     assert len(pl) == len(pe) == L + 1

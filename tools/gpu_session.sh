@@ -29,6 +29,7 @@ has bench && step bench 600 python bench.py
 has e2e && step e2e_probe 900 python tools/e2e_probe.py
 has probe && step line_probe 300 python tools/line_probe.py
 has lprobe && step lookup_probe 300 python tools/lookup_probe.py
+has gprobe && step gather_probe 300 python tools/gather_probe.py
 has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
 has ablateb && step ablate_bwd 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --bwd
 has ablatec && step ablate_conv 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --convc1

@@ -2,8 +2,8 @@
 
     python tools/lookup_probe.py [--config sceneflow] [--reps 5]
 
-The chain lookup (product) and the per-level lookup are event-timed per
-launch, 32 launches back to back like the bench, under coordinate
+The block's default lookup (the pair kernel for 4 fp32 levels), the
+level-1 chain kernel and the per-level lookup are event-timed per launch, 32 launches back to back like the bench, under coordinate
 distributions that differ only in locality:
   bench   coords_grid - U[0,64) per pixel, a fresh draw per launch (bench.py);
   same    one bench draw reused by all 32 launches (upper bound on re-use);
@@ -82,7 +82,9 @@ def main():
         pyr = blk.corr_pyramid
         for kind in ("bench", "same", "row", "smooth"):
             cs = coords_sets(B, H, W1, W2, iters, kind, dev)
-            for name, fn in (("chain", blk), ("per_level", lambda c: rcorr.lookup(pyr, c, L, r))):
+            l1 = pyr[:2] + [None] * (L - 2)
+            for name, fn in (("default", blk), ("chain_l1", lambda c: rcorr.lookup_chain(l1, c, L, r)),
+                             ("per_level", lambda c: rcorr.lookup(pyr, c, L, r))):
                 us = time_seq(fn, cs, a.reps)
                 res[f"{kind}/{name}"] = {"us": round(us, 2),
                                          "alg_GBps": round(lbytes / (us * 1e-6) / 1e9, 1)}

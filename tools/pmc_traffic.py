@@ -56,7 +56,8 @@ def main():
     kw = GiB / (cal_w[0] * 1024) if cal_w else 1.0
     res = {}
     for kname, key in (("build", "build_"), ("lookup", "lookup_kernel"),
-                       ("lookup_chain", "lookup_chain_kernel"), ("lookup_bwd", "lookup_bwd_pre_kernel")):
+                       ("lookup_chain", "lookup_chain_kernel"), ("lookup_pair", "lookup_pair_kernel"),
+                       ("lookup_bwd", "lookup_bwd_pre_kernel")):
         f = per_kernel(fr, key)
         w = per_kernel(wr, key)
         if f is None or w is None:

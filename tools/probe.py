@@ -4,7 +4,8 @@
 
 Launches, in order: a calibration copy (torch clone of a 1 GiB fp32 tensor:
 exactly 1 GiB read + 1 GiB written), N builds (rc::build_f32_ring_kernel), N
-CorrBlock1D lookups (rc::lookup_chain_kernel) and N per-level lookups (rc::lookup_kernel) and N lookup backwards
+CorrBlock1D lookups (rc::lookup_pair_kernel for 4 fp32 levels), N per-level lookups
+(rc::lookup_kernel), N level-1 chain lookups (rc::lookup_chain_kernel), N lookup backwards
 (rc::lookup_bwd_pre_kernel) of bench.py's workload.  tools/pmc_traffic.py turns
 the per-dispatch FETCH_SIZE / WRITE_SIZE into bytes per launch.
 """
@@ -43,6 +44,10 @@ def main():
             blk(coords[it % iters])        # rc::lookup_chain_kernel (fp32) / lookup_kernel
         for it in range(a.iters):          # the per-level kernel on the same pyramid
             rcorr.lookup(blk.corr_pyramid, coords[it % iters], L, r)
+        if pdt == torch.float32 and L in (3, 4):   # the level-1 chain kernel (levels 0-1 given)
+            lv = blk.corr_pyramid[:2] + [None] * (L - 2)
+            for it in range(a.iters):
+                rcorr.lookup_chain(lv, coords[it % iters], L, r)
         if pdt == torch.float32:           # rc::lookup_bwd_pre_kernel (one per lookup call)
             P = B * H * W1
             grads = rcorr.grad_buffers(P, [W2 >> i for i in range(L)], dev)
