@@ -512,8 +512,13 @@ __device__ __forceinline__ void window_taps(const float *w, float xl, float nwin
         const float w1 = xp - x0, w0 = 1.0f - w1;
         const float nt = nwin + (float)(t - R);
         const bool lo_ = x0 < nt, hi_ = x0 > nt;
-        const float v0 = lo_ ? w[t] : (hi_ ? w[t + 2] : w[t + 1]);
-        const float v1 = lo_ ? w[t + 1] : (hi_ ? w[t + 3] : w[t + 2]);
+        // opaque copies: the selects must stay selects of registers (folded
+        // into a load from a select of addresses, the window goes to scratch
+        // memory: 112 B/lane and 87 instead of 14 vector loads per wave)
+        float e0 = w[t], e1 = w[t + 1], e2 = w[t + 2], e3 = w[t + 3];
+        asm("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3));
+        const float v0 = lo_ ? e0 : (hi_ ? e2 : e1);
+        const float v1 = lo_ ? e1 : (hi_ ? e3 : e2);
         bad |= chk && !(fabsf(x0 - nt) <= 1.0f);
         res[t] = fmaf(w1, v1, w0 * v0);
     }
@@ -540,7 +545,7 @@ __device__ __forceinline__ void level_taps_mem(const float *row, float xl, int W
     }
 }
 
-template <int R, class Sink>
+template <int R, bool NOFALLBACK = false, class Sink>
 __device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupArgs &a, int lo,
                                             float x, long long pp, Sink &&sink) {
     typedef PairSpan<R> PS;
@@ -569,7 +574,7 @@ __device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupA
     bool bad = !ps.valid && ps.inwin;
     window_taps<R>(weven, xlo, ps.n, Wlo, ps.inwin, r0, bad);
     window_taps<R>(wodd, xhi, ps.m, Whi, ps.inwin, r1, bad);
-    if (__builtin_expect(bad, 0)) {   // one wave-level check for the pair
+    if (!NOFALLBACK && __builtin_expect(bad, 0)) {   // one wave-level check for the pair
         const float *row = static_cast<const float *>(a.lvl[lo]) + pp * a.ld[lo];
         level_taps_mem<R, 1>(row, xlo, Wlo, r0);
         level_taps_mem<R, 2>(row, xhi, Whi, r1);
@@ -581,7 +586,9 @@ __device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupA
 }
 
 // NL = 2 (levels 0-1) or 4 (levels 0-3; level 2 stored, levels 1 and 3 derived).
-template <int R, int NL>
+// M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-203, dev library):
+// 1 = no output stores, 2 = no fallback path, 3 = span loads only.
+template <int R, int NL, int M = 0>
 __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
     const long long pblk = (long long)blockIdx.x * 256;
@@ -593,23 +600,48 @@ __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     float *outp = a.out + bimg * (long long)(NL * (2 * R + 1)) * a.HW + rem;
     const long long lrow = pp - pblk;
     auto sink = [&](int ch, float v) {
-        if (active) outp[(long long)ch * a.HW] = v;
+        if (active && (M != 1 || v == 1234.5f)) outp[(long long)ch * a.HW] = v;
     };
     PairSpan<R> s0;
     issue_pair<R>(s0, a, 0, x, pblk, lrow);
+    if constexpr (M == 3) {
+        uint32_t acc = 0;
+        PairSpan<R> s2;
+        if constexpr (NL == 4) issue_pair<R>(s2, a, 2, x, pblk, lrow);
+#pragma unroll
+        for (int k = 0; k < PairSpan<R>::NC; ++k)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                acc ^= __builtin_bit_cast(uint32_t, s0.q[k][c]);
+                if constexpr (NL == 4) acc ^= __builtin_bit_cast(uint32_t, s2.q[k][c]);
+            }
+        if (acc == 0x12345678u) outp[0] = 0.0f;
+        return;
+    }
     if constexpr (NL == 4) {
         PairSpan<R> s2;
         issue_pair<R>(s2, a, 2, x, pblk, lrow);
-        finish_pair<R>(s0, a, 0, x, pp, sink);
-        finish_pair<R>(s2, a, 2, x, pp, sink);
+        finish_pair<R, M == 2>(s0, a, 0, x, pp, sink);
+        finish_pair<R, M == 2>(s2, a, 2, x, pp, sink);
     } else {
-        finish_pair<R>(s0, a, 0, x, pp, sink);
+        finish_pair<R, M == 2>(s0, a, 0, x, pp, sink);
     }
 }
 
 template <int R>
 static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
+#ifdef RAFTCORR_DEV
+    if constexpr (R == 4) {
+        const int v = dev_knob("RAFTCORR_LOOKUP_VARIANT");
+        if (a.levels == 4 && v >= 201 && v <= 203) {
+            if (v == 201) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 202) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 203) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
+            return hipGetLastError();
+        }
+    }
+#endif
     if (a.levels == 4)
         hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
     else if (a.levels == 2)

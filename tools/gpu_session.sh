@@ -28,7 +28,7 @@ has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has bench && step bench 600 python bench.py
 has e2e && step e2e_probe 900 python tools/e2e_probe.py
 has probe && step line_probe 300 python tools/line_probe.py
-has lprobe && step lookup_probe 300 python tools/lookup_probe.py
+has lprobe && step lookup_probe 300 python tools/lookup_probe.py --dev-variants ${LPROBE_VARIANTS:-201,202,203,101,102,103,104}
 has gprobe && step gather_probe 300 python tools/gather_probe.py
 has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
 has ablateb && step ablate_bwd 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --bwd

@@ -70,6 +70,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="sceneflow")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--dev-variants", default="",
+                    help="RAFTCORR_LOOKUP_VARIANT values to time on the bench coords "
+                         "(libraftcorr_dev.so)")
     a = ap.parse_args()
     B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -88,6 +91,18 @@ def main():
                 us = time_seq(fn, cs, a.reps)
                 res[f"{kind}/{name}"] = {"us": round(us, 2),
                                          "alg_GBps": round(lbytes / (us * 1e-6) / 1e9, 1)}
+        if a.dev_variants:
+            from raft_stereo_amd import _lib
+            cs = coords_sets(B, H, W1, W2, iters, "bench", dev)
+            l1 = pyr[:2] + [None] * (L - 2)
+            with _lib.dev_library():
+                for v in ["0"] + a.dev_variants.split(","):
+                    os.environ["RAFTCORR_LOOKUP_VARIANT"] = v
+                    for name, fn in (("default", blk),
+                                     ("chain_l1", lambda c: rcorr.lookup_chain(l1, c, L, r))):
+                        us = time_seq(fn, cs, a.reps)
+                        res[f"dev{v}/{name}"] = {"us": round(us, 2)}
+            os.environ["RAFTCORR_LOOKUP_VARIANT"] = "0"
     print(json.dumps(res, indent=1))
 
 
