@@ -410,7 +410,7 @@ class CorrBlock1D:
         # default on in that case): same values, same shapes, pooled by the
         # same fp32 ops.
         self._chain = (pyramid_dtype == torch.float32 and num_levels in (2, 3, 4)
-                       and 1 <= radius <= 4)
+                       and 1 <= radius <= 4 and fmap2.shape[-1] <= 65536)
         lazy = self._chain if lazy_levels is None else (bool(lazy_levels) and self._chain)
         with torch.no_grad():
             if lazy and num_levels == 3:

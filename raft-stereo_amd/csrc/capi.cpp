@@ -191,6 +191,10 @@ int chain_kind(const char *who, const void *const *pyr, const int *widths, int l
             return fail(RC_EINVAL, "%s: width %d of level %d is not floor(%d/2)", who, widths[i], i,
                         widths[i - 1]);
     *pair = levels == 2 || (levels == 4 && pyr[2] != nullptr);
+    // the pair kernel's window argument holds for widths up to 2^16 (lookup.hip)
+    if (*pair && widths[0] > 65536)
+        return fail(RC_EUNSUPPORTED, "%s: level-0 width %d > 65536 for the pair kernel", who,
+                    widths[0]);
     if (!*pair && !pyr[1])
         return fail(RC_EINVAL, "%s: %d levels need level 1 (or level 2 with 4 levels)", who, levels);
     if (!*pair && levels < 3)

@@ -494,12 +494,20 @@ __device__ __forceinline__ void issue_pair(PairSpan<R> &ps, const LookupArgs &a,
     }
 }
 
-// Taps of one level from its zero-padded window w[NW] (element nwin-R-1+jj):
-// the reference's fp32 sequence (see lookup_kernel); `bad` flags a tap whose
-// floor left the window (unreachable within the division's error bound).
+// Taps of one level from its zero-padded window w[NW] (element nwin-R-1+jj),
+// the reference's fp32 sequence (see lookup_kernel).  No per-tap check that
+// the tap's floor stayed in the window is needed here, because it cannot leave
+// it: for a lane in the window's range (|xl| < W + R + 4) and W <= 2^16,
+//  (1) xt = fl(xl + k) lies in [m, m + 1] with m = floor(xl) + k = nt
+//      (integers are representable and rounding is monotone);
+//  (2) the round trip xp = fl(fl(fl(fl(2 xt)/(W-1)) - 1) + 1) * (W-1)/2
+//      differs from xt by at most (4|xt| + 1.5(W-1)) 2^-24 < 0.03;
+// so x0 = floor(xp) is nt - 1, nt or nt + 1 (nt + 2 would need xt = nt + 1
+// and an error >= 1), i.e. taps x0 and x0 + 1 are window elements t..t+3.
+// The C-ABI rejects wider levels for this kernel (include/raftcorr.h).
 template <int R>
-__device__ __forceinline__ void window_taps(const float *w, float xl, float nwin, int W, bool chk,
-                                            float *res, bool &bad) {
+__device__ __forceinline__ void window_taps(const float *w, float xl, float nwin, int W,
+                                            float *res) {
     constexpr int T = 2 * R + 1;
     const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
     const DivRN dv = div_prep(Wm1);
@@ -519,13 +527,13 @@ __device__ __forceinline__ void window_taps(const float *w, float xl, float nwin
         asm("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3));
         const float v0 = lo_ ? e0 : (hi_ ? e2 : e1);
         const float v1 = lo_ ? e1 : (hi_ ? e3 : e2);
-        bad |= chk && !(fabsf(x0 - nt) <= 1.0f);
         res[t] = fmaf(w1, v1, w0 * v0);
     }
 }
 
-// The (unreachable within the error bound) memory path for one level: every
-// tap re-read, level-i element k = pool of S consecutive span-level elements.
+// The memory path for a lane whose level pair breaks the span relation
+// n = 2m + dd (only a subnormal x can): every tap re-read, level-i element k
+// = pool of S consecutive span-level elements.
 template <int R, int S>
 __device__ __forceinline__ void level_taps_mem(const float *row, float xl, int W, float *res) {
     constexpr int T = 2 * R + 1;
@@ -571,10 +579,9 @@ __device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupA
     }
     const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
     float r0[T], r1[T];
-    bool bad = !ps.valid && ps.inwin;
-    window_taps<R>(weven, xlo, ps.n, Wlo, ps.inwin, r0, bad);
-    window_taps<R>(wodd, xhi, ps.m, Whi, ps.inwin, r1, bad);
-    if (!NOFALLBACK && __builtin_expect(bad, 0)) {   // one wave-level check for the pair
+    window_taps<R>(weven, xlo, ps.n, Wlo, r0);
+    window_taps<R>(wodd, xhi, ps.m, Whi, r1);
+    if (!NOFALLBACK && __builtin_expect(ps.inwin && !ps.valid, 0)) {   // subnormal x only
         const float *row = static_cast<const float *>(a.lvl[lo]) + pp * a.ld[lo];
         level_taps_mem<R, 1>(row, xlo, Wlo, r0);
         level_taps_mem<R, 2>(row, xhi, Whi, r1);
@@ -585,46 +592,67 @@ __device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupA
     for (int t = 0; t < T; ++t) sink((lo + 1) * T + t, r1[t]);
 }
 
+// One lane's pixel of one group: index, x, output pointer, rsrc base row.
+struct PairPixel {
+    long long pblk, pp, lrow;
+    float *outp;
+    float x;
+    bool active;
+};
+
+template <int R, int NL>
+__device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long pblk) {
+    PairPixel q;
+    q.pblk = pblk;
+    const long long p = pblk + threadIdx.x;
+    q.active = p < a.P;
+    q.pp = q.active ? p : a.P - 1;
+    const long long bimg = q.pp / a.HW, rem = q.pp - bimg * a.HW;
+    q.x = pixel_x(a, bimg, rem, q.active);
+    q.outp = a.out + bimg * (long long)(NL * (2 * R + 1)) * a.HW + rem;
+    q.lrow = q.pp - pblk;
+    return q;
+}
+
 // NL = 2 (levels 0-1) or 4 (levels 0-3; level 2 stored, levels 1 and 3 derived).
+// G pixel groups per lane (block b: pixels b*256G + 256g + lane): every
+// group's span loads issue first, then group g's math and stores run while
+// the loads of groups > g are still in flight.
 // M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-203, dev library):
 // 1 = no output stores, 2 = no fallback path, 3 = span loads only.
-template <int R, int NL, int M = 0>
+template <int R, int NL, int M = 0, int G = 1>
 __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
-    const long long pblk = (long long)blockIdx.x * 256;
-    const long long p = pblk + threadIdx.x;
-    const bool active = p < a.P;
-    const long long pp = active ? p : a.P - 1;
-    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
-    const float x = pixel_x(a, bimg, rem, active);
-    float *outp = a.out + bimg * (long long)(NL * (2 * R + 1)) * a.HW + rem;
-    const long long lrow = pp - pblk;
-    auto sink = [&](int ch, float v) {
-        if (active && (M != 1 || v == 1234.5f)) outp[(long long)ch * a.HW] = v;
-    };
-    PairSpan<R> s0;
-    issue_pair<R>(s0, a, 0, x, pblk, lrow);
+    constexpr int NP = NL / 2;                        // spans per pixel
+    PairPixel px[G];
+    PairSpan<R> sp[G][NP];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        px[g] = pair_pixel<R, NL>(a, ((long long)blockIdx.x * G + g) * 256);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) issue_pair<R>(sp[g][k], a, 2 * k, px[g].x, px[g].pblk, px[g].lrow);
+    }
     if constexpr (M == 3) {
         uint32_t acc = 0;
-        PairSpan<R> s2;
-        if constexpr (NL == 4) issue_pair<R>(s2, a, 2, x, pblk, lrow);
 #pragma unroll
-        for (int k = 0; k < PairSpan<R>::NC; ++k)
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                acc ^= __builtin_bit_cast(uint32_t, s0.q[k][c]);
-                if constexpr (NL == 4) acc ^= __builtin_bit_cast(uint32_t, s2.q[k][c]);
-            }
-        if (acc == 0x12345678u) outp[0] = 0.0f;
+            for (int k = 0; k < NP; ++k)
+#pragma unroll
+                for (int c = 0; c < PairSpan<R>::NC; ++c)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc ^= __builtin_bit_cast(uint32_t, sp[g][k].q[c][e]);
+        if (acc == 0x12345678u) a.out[0] = 0.0f;
         return;
     }
-    if constexpr (NL == 4) {
-        PairSpan<R> s2;
-        issue_pair<R>(s2, a, 2, x, pblk, lrow);
-        finish_pair<R, M == 2>(s0, a, 0, x, pp, sink);
-        finish_pair<R, M == 2>(s2, a, 2, x, pp, sink);
-    } else {
-        finish_pair<R, M == 2>(s0, a, 0, x, pp, sink);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const PairPixel &q = px[g];
+        auto sink = [&](int ch, float v) {
+            if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
+        };
+#pragma unroll
+        for (int k = 0; k < NP; ++k) finish_pair<R, M == 2>(sp[g][k], a, 2 * k, q.x, q.pp, sink);
     }
 }
 
@@ -634,10 +662,15 @@ static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
 #ifdef RAFTCORR_DEV
     if constexpr (R == 4) {
         const int v = dev_knob("RAFTCORR_LOOKUP_VARIANT");
-        if (a.levels == 4 && v >= 201 && v <= 203) {
+        const unsigned nblk2 = (unsigned)((a.P + 511) / 512);
+        if (a.levels == 4 && v >= 201 && v <= 206) {
             if (v == 201) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 202) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 203) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
+            // two pixel groups per lane: product math / no stores / loads only
+            if (v == 204) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, 2>), dim3(nblk2), dim3(256), 0, s, a);
+            if (v == 205) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1, 2>), dim3(nblk2), dim3(256), 0, s, a);
+            if (v == 206) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3, 2>), dim3(nblk2), dim3(256), 0, s, a);
             return hipGetLastError();
         }
     }
