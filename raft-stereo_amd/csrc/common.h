@@ -110,6 +110,7 @@ struct LookupArgs {
     const float *delta;
     float *coords_out;
     float *flow_out;
+    unsigned long long *dbg;  // dev library only: per-wave timeline stamps (else null)
 };
 
 // Backward of the lookup: level gradients (fp32, row stride ld[i] % 4 == 0).

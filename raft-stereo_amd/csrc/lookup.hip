@@ -614,16 +614,54 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
     return q;
 }
 
+// Output of one level pair through LDS: the wave's 64 pixels x 2(2r+1)
+// channels are written to a per-wave LDS tile [channel][pixel] (one
+// ds_write_b32 per channel, conflict-free) and stored as 16-B vectors of 4
+// consecutive pixels of one channel: (2(2r+1) * 64 / 4) / 64 = (2r+1)/2
+// dwordx4 stores per lane instead of 2(2r+1) dword stores.  Vector-memory
+// issue, not bytes, bounds this kernel, and an output
+// store costs the same issue slot whatever its width.  Needs H*W1 % 4 == 0
+// (a 4-pixel group never straddles an image) -- the launcher checks.
+template <int R>
+struct PairTile {
+    static constexpr int CH = 2 * (2 * R + 1);        // channels of one level pair
+    static constexpr int QUADS = CH * 16;             // 16-B vectors per wave
+    float *t;                                         // this wave's [CH][64] tile
+};
+
+template <int R>
+__device__ __forceinline__ void pair_tile_store(const PairTile<R> &tl, const LookupArgs &a,
+                                                long long pwave, int lo, int NLT) {
+    typedef PairTile<R> PT;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < (PT::QUADS + 63) / 64; ++j) {
+        const int qd = j * 64 + lane;
+        if (PT::QUADS % 64 != 0 && qd >= PT::QUADS) break;
+        const int c = qd >> 4, pq = qd & 15;
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(tl.t + c * 64 + 4 * pq);
+        const long long p = pwave + 4 * pq;
+        if (p < a.P) {
+            const long long bimg = p / a.HW, rem = p - bimg * a.HW;
+            *reinterpret_cast<f32x4 *>(a.out + (bimg * NLT + lo * (2 * R + 1) + c) * a.HW + rem) = v;
+        }
+    }
+}
+
 // NL = 2 (levels 0-1) or 4 (levels 0-3; level 2 stored, levels 1 and 3 derived).
 // G pixel groups per lane (block b: pixels b*256G + 256g + lane): every
 // group's span loads issue first, then group g's math and stores run while
-// the loads of groups > g are still in flight.
+// the loads of groups > g are still in flight.  WIDE: 16-B output stores
+// through a per-wave LDS tile (pair_tile_store), G = 1 only.
 // M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-203, dev library):
 // 1 = no output stores, 2 = no fallback path, 3 = span loads only.
-template <int R, int NL, int M = 0, int G = 1>
+template <int R, int NL, int M = 0, int G = 1, bool WIDE = false>
 __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
+    static_assert(!WIDE || G == 1, "wide stores: one group per lane");
     constexpr int NP = NL / 2;                        // spans per pixel
+    constexpr int T = 2 * R + 1;
+    __shared__ __attribute__((aligned(16))) float tiles[WIDE ? 4 : 1][WIDE ? PairTile<R>::CH * 64 : 1];
     PairPixel px[G];
     PairSpan<R> sp[G][NP];
 #pragma unroll
@@ -645,6 +683,21 @@ __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
         if (acc == 0x12345678u) a.out[0] = 0.0f;
         return;
     }
+    if constexpr (WIDE) {
+        const PairPixel &q = px[0];
+        PairTile<R> tl{tiles[threadIdx.x >> 6]};
+        const int lane = threadIdx.x & 63;
+        const long long pwave = q.pblk + (threadIdx.x & ~63);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            // the LDS tile is private to the wave and LDS runs a wave's
+            // operations in order: no barrier between the writes and reads
+            auto sink = [&](int ch, float v) { tl.t[(ch - 2 * k * T) * 64 + lane] = v; };
+            finish_pair<R, M == 2>(sp[0][k], a, 2 * k, q.x, q.pp, sink);
+            if constexpr (M != 1) pair_tile_store<R>(tl, a, pwave, 2 * k, NL * T);
+        }
+        return;
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const PairPixel &q = px[g];
@@ -656,6 +709,54 @@ __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     }
 }
 
+#ifdef RAFTCORR_DEV
+__device__ __forceinline__ unsigned long long rtc_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+// Diagnostic build of the 4-level pair kernel (dev library, variant 210):
+// lane 0 of every wave records s_memrealtime (100 MHz) at
+//   0 start, 1 loads issued, 2 span 0 landed, 3 pair 0 done (math + stores
+//   issued), 4 span 2 landed, 5 pair 2 done, 6 all stores drained,
+// plus HW_ID, into dbg[wave * 8 + k].  Its run time is not the product's
+// (the waits forbid overlaps); read shares and distributions only.
+template <int R>
+__global__ __launch_bounds__(256) void lookup_pair_stamped_kernel(LookupArgs a) {
+    unsigned long long st[7];
+    st[0] = rtc_stamp();
+    const PairPixel q = pair_pixel<R, 4>(a, (long long)blockIdx.x * 256);
+    PairSpan<R> s0, s2;
+    issue_pair<R>(s0, a, 0, q.x, q.pblk, q.lrow);
+    issue_pair<R>(s2, a, 2, q.x, q.pblk, q.lrow);
+    st[1] = rtc_stamp();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PairSpan<R>::NC) : "memory");
+    st[2] = rtc_stamp();
+    auto sink = [&](int ch, float v) {
+        if (q.active) q.outp[(long long)ch * a.HW] = v;
+    };
+    finish_pair<R>(s0, a, 0, q.x, q.pp, sink);
+    st[3] = rtc_stamp();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (2 * R + 1)) : "memory");
+    st[4] = rtc_stamp();
+    finish_pair<R>(s2, a, 2, q.x, q.pp, sink);
+    st[5] = rtc_stamp();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[6] = rtc_stamp();
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long *d = a.dbg + ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[k] = st[k];
+        d[7] = hw;
+    }
+}
+#endif
+
 template <int R>
 static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
@@ -663,6 +764,18 @@ static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
     if constexpr (R == 4) {
         const int v = dev_knob("RAFTCORR_LOOKUP_VARIANT");
         const unsigned nblk2 = (unsigned)((a.P + 511) / 512);
+        if (a.levels == 4 && v == 210 && a.dbg) {
+            hipLaunchKernelGGL((lookup_pair_stamped_kernel<R>), dim3(nblk), dim3(256), 0, s, a);
+            return hipGetLastError();
+        }
+        if (a.levels == 4 && v == 220) {   // dword output stores (pre-LDS-tile product)
+            hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+            return hipGetLastError();
+        }
+        if (a.levels == 4 && v == 221 && a.HW % 4 == 0) {   // wide stores, no output stores
+            hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+            return hipGetLastError();
+        }
         if (a.levels == 4 && v >= 201 && v <= 206) {
             if (v == 201) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 202) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2>), dim3(nblk), dim3(256), 0, s, a);
@@ -675,12 +788,16 @@ static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
         }
     }
 #endif
-    if (a.levels == 4)
-        hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
-    else if (a.levels == 2)
-        hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
-    else
+    const bool wide = a.HW % 4 == 0;
+    if (a.levels == 4) {
+        if (wide) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+    } else if (a.levels == 2) {
+        if (wide) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+    } else {
         return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ has e2e && step e2e_probe 900 python tools/e2e_probe.py
 has probe && step line_probe 300 python tools/line_probe.py
 has lprobe && step lookup_probe 300 python tools/lookup_probe.py --dev-variants ${LPROBE_VARIANTS:-201,202,203,101,102,103,104}
 has gprobe && step gather_probe 300 python tools/gather_probe.py
+has timeline && step lookup_timeline 300 python tools/lookup_timeline.py
 has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
 has ablateb && step ablate_bwd 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --bwd
 has ablatec && step ablate_conv 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --convc1
