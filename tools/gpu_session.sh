@@ -61,16 +61,16 @@ if has pmcsq; then
 fi
 if has pmcw; then   # wave-state breakdown: where each kernel's wave cycles go
     step pmc_w1 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE \
-        --output-format csv -d "$OUT/pmc_w1" -o s -- python3 tools/probe.py
+        --output-format csv -d "$OUT/pmc_w1" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
     step pmc_w2 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_INSTS_LDS \
-        --output-format csv -d "$OUT/pmc_w2" -o s -- python3 tools/probe.py
+        --output-format csv -d "$OUT/pmc_w2" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
     python tools/pmc_raw.py "$OUT/pmc_w1" > "$OUT/pmc_w.txt" 2>&1; python tools/pmc_raw.py "$OUT/pmc_w2" >> "$OUT/pmc_w.txt" 2>&1; grep lookup "$OUT/pmc_w.txt"
 fi
 if has pmcv; then
     step pmc_v1 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_VMEM_TA_ADDR_FIFO_FULL SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
-        --output-format csv -d "$OUT/pmc_v1" -o s -- python3 tools/probe.py
+        --output-format csv -d "$OUT/pmc_v1" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
     step pmc_v2 120 rocprofv3 --pmc TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES TCP_TCC_READ_REQ_LATENCY TCP_TCC_READ_REQ TCP_TCP_TA_ADDR_STALL_CYCLES SQ_INSTS_VALU_TRANS_F32 SQ_THREAD_CYCLES_VALU \
-        --output-format csv -d "$OUT/pmc_v2" -o s -- python3 tools/probe.py
+        --output-format csv -d "$OUT/pmc_v2" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
     python tools/pmc_raw.py "$OUT/pmc_v1" > "$OUT/pmc_v.txt" 2>&1; python tools/pmc_raw.py "$OUT/pmc_v2" >> "$OUT/pmc_v.txt" 2>&1; cat "$OUT/pmc_v.txt"
 fi
 exit 0

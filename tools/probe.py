@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--config", default="sceneflow")
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--pyr-dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--dev-variants", default="",
+                    help="also run N lookups per RAFTCORR_LOOKUP_VARIANT value through "
+                         "libraftcorr_dev.so (their kernels carry distinct template names)")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
     B, D, H, W1, W2, L, r, iters, _ = cfg
@@ -54,6 +57,14 @@ def main():
             go = torch.randn(B, L * (2 * r + 1), H, W1, device=dev)
             for it in range(a.iters):
                 rcorr.lookup_backward(grads, coords[it % iters], go, L, r)
+        if a.dev_variants:
+            from raft_stereo_amd import _lib
+            with _lib.dev_library():
+                for v in a.dev_variants.split(","):
+                    os.environ["RAFTCORR_LOOKUP_VARIANT"] = v
+                    for it in range(a.iters):
+                        blk(coords[it % iters])
+                os.environ["RAFTCORR_LOOKUP_VARIANT"] = "0"
         torch.cuda.synchronize()
     print("probe done")
 
