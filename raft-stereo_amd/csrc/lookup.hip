@@ -614,99 +614,27 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
     return q;
 }
 
-// Output of one level pair through LDS: the wave's 64 pixels x 2(2r+1)
-// channels are written to a per-wave LDS tile [channel][pixel] (one
-// ds_write_b32 per channel, conflict-free) and stored as 16-B vectors of 4
-// consecutive pixels of one channel: (2(2r+1) * 64 / 4) / 64 = (2r+1)/2
-// dwordx4 stores per lane instead of 2(2r+1) dword stores.  Vector-memory
-// issue, not bytes, bounds this kernel, and an output
-// store costs the same issue slot whatever its width.  Needs H*W1 % 4 == 0
-// (a 4-pixel group never straddles an image) -- the launcher checks.
-template <int R>
-struct PairTile {
-    static constexpr int CH = 2 * (2 * R + 1);        // channels of one level pair
-    static constexpr int QUADS = CH * 16;             // 16-B vectors per wave
-    float *t;                                         // this wave's [CH][64] tile
-};
-
-template <int R>
-__device__ __forceinline__ void pair_tile_store(const PairTile<R> &tl, const LookupArgs &a,
-                                                long long pwave, int lo, int NLT) {
-    typedef PairTile<R> PT;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int j = 0; j < (PT::QUADS + 63) / 64; ++j) {
-        const int qd = j * 64 + lane;
-        if (PT::QUADS % 64 != 0 && qd >= PT::QUADS) break;
-        const int c = qd >> 4, pq = qd & 15;
-        const f32x4 v = *reinterpret_cast<const f32x4 *>(tl.t + c * 64 + 4 * pq);
-        const long long p = pwave + 4 * pq;
-        if (p < a.P) {
-            const long long bimg = p / a.HW, rem = p - bimg * a.HW;
-            *reinterpret_cast<f32x4 *>(a.out + (bimg * NLT + lo * (2 * R + 1) + c) * a.HW + rem) = v;
-        }
-    }
-}
-
 // NL = 2 (levels 0-1) or 4 (levels 0-3; level 2 stored, levels 1 and 3 derived).
-// G pixel groups per lane (block b: pixels b*256G + 256g + lane): every
-// group's span loads issue first, then group g's math and stores run while
-// the loads of groups > g are still in flight.  WIDE: 16-B output stores
-// through a per-wave LDS tile (pair_tile_store), G = 1 only.
-// M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-203, dev library):
-// 1 = no output stores, 2 = no fallback path, 3 = span loads only.
-template <int R, int NL, int M = 0, int G = 1, bool WIDE = false>
+// Both spans' loads issue first; pair 0's math and stores run while pair 2's
+// loads are in flight.  Measured and not kept: 16-B output
+// stores through a per-wave LDS tile (9 instead of 36 store instructions per
+// wave: 26.0 vs 25.8 us), two pixels per lane with both pixels' loads in
+// flight (26.6 us, 198 VGPRs).
+// M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-202, dev library):
+// 1 = no output stores, 2 = no fallback path.
+template <int R, int NL, int M = 0>
 __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
-    static_assert(!WIDE || G == 1, "wide stores: one group per lane");
     constexpr int NP = NL / 2;                        // spans per pixel
-    constexpr int T = 2 * R + 1;
-    __shared__ __attribute__((aligned(16))) float tiles[WIDE ? 4 : 1][WIDE ? PairTile<R>::CH * 64 : 1];
-    PairPixel px[G];
-    PairSpan<R> sp[G][NP];
+    const PairPixel q = pair_pixel<R, NL>(a, (long long)blockIdx.x * 256);
+    PairSpan<R> sp[NP];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        px[g] = pair_pixel<R, NL>(a, ((long long)blockIdx.x * G + g) * 256);
+    for (int k = 0; k < NP; ++k) issue_pair<R>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
+    auto sink = [&](int ch, float v) {
+        if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
+    };
 #pragma unroll
-        for (int k = 0; k < NP; ++k) issue_pair<R>(sp[g][k], a, 2 * k, px[g].x, px[g].pblk, px[g].lrow);
-    }
-    if constexpr (M == 3) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-#pragma unroll
-                for (int c = 0; c < PairSpan<R>::NC; ++c)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) acc ^= __builtin_bit_cast(uint32_t, sp[g][k].q[c][e]);
-        if (acc == 0x12345678u) a.out[0] = 0.0f;
-        return;
-    }
-    if constexpr (WIDE) {
-        const PairPixel &q = px[0];
-        PairTile<R> tl{tiles[threadIdx.x >> 6]};
-        const int lane = threadIdx.x & 63;
-        const long long pwave = q.pblk + (threadIdx.x & ~63);
-#pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            // the LDS tile is private to the wave and LDS runs a wave's
-            // operations in order: no barrier between the writes and reads
-            auto sink = [&](int ch, float v) { tl.t[(ch - 2 * k * T) * 64 + lane] = v; };
-            finish_pair<R, M == 2>(sp[0][k], a, 2 * k, q.x, q.pp, sink);
-            if constexpr (M != 1) pair_tile_store<R>(tl, a, pwave, 2 * k, NL * T);
-        }
-        return;
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const PairPixel &q = px[g];
-        auto sink = [&](int ch, float v) {
-            if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
-        };
-#pragma unroll
-        for (int k = 0; k < NP; ++k) finish_pair<R, M == 2>(sp[g][k], a, 2 * k, q.x, q.pp, sink);
-    }
+    for (int k = 0; k < NP; ++k) finish_pair<R, M == 2>(sp[k], a, 2 * k, q.x, q.pp, sink);
 }
 
 #ifdef RAFTCORR_DEV
@@ -763,41 +691,23 @@ static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
 #ifdef RAFTCORR_DEV
     if constexpr (R == 4) {
         const int v = dev_knob("RAFTCORR_LOOKUP_VARIANT");
-        const unsigned nblk2 = (unsigned)((a.P + 511) / 512);
         if (a.levels == 4 && v == 210 && a.dbg) {
             hipLaunchKernelGGL((lookup_pair_stamped_kernel<R>), dim3(nblk), dim3(256), 0, s, a);
             return hipGetLastError();
         }
-        if (a.levels == 4 && v == 220) {   // dword output stores (pre-LDS-tile product)
-            hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
-            return hipGetLastError();
-        }
-        if (a.levels == 4 && v == 221 && a.HW % 4 == 0) {   // wide stores, no output stores
-            hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-            return hipGetLastError();
-        }
-        if (a.levels == 4 && v >= 201 && v <= 206) {
+        if (a.levels == 4 && (v == 201 || v == 202)) {
             if (v == 201) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 202) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 203) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
-            // two pixel groups per lane: product math / no stores / loads only
-            if (v == 204) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, 2>), dim3(nblk2), dim3(256), 0, s, a);
-            if (v == 205) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1, 2>), dim3(nblk2), dim3(256), 0, s, a);
-            if (v == 206) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3, 2>), dim3(nblk2), dim3(256), 0, s, a);
             return hipGetLastError();
         }
     }
 #endif
-    const bool wide = a.HW % 4 == 0;
-    if (a.levels == 4) {
-        if (wide) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
-    } else if (a.levels == 2) {
-        if (wide) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
-    } else {
+    if (a.levels == 4)
+        hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+    else if (a.levels == 2)
+        hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+    else
         return hipErrorInvalidValue;
-    }
     return hipGetLastError();
 }
 

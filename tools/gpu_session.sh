@@ -28,7 +28,7 @@ has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has bench && step bench 600 python bench.py
 has e2e && step e2e_probe 900 python tools/e2e_probe.py
 has probe && step line_probe 300 python tools/line_probe.py
-has lprobe && step lookup_probe 300 python tools/lookup_probe.py --dev-variants ${LPROBE_VARIANTS:-201,202,203,101,102,103,104}
+has lprobe && step lookup_probe 300 python tools/lookup_probe.py --dev-variants ${LPROBE_VARIANTS:-201,202}
 has gprobe && step gather_probe 300 python tools/gather_probe.py
 has timeline && step lookup_timeline 300 python tools/lookup_timeline.py
 has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
@@ -53,6 +53,7 @@ if has pmc; then
         --output-format csv -d "$OUT/pmc_sq" -o s -- python3 tools/probe.py
     python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --out "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
     cat "$OUT/traffic.log"
+    python tools/pmc_sq.py "$OUT/pmc_sq" > "$OUT/pmc_sq.txt" 2>&1; cat "$OUT/pmc_sq.txt"
 fi
 if has pmcsq; then
     step pmc_sq2 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE \

@@ -57,6 +57,8 @@ def main():
             go = torch.randn(B, L * (2 * r + 1), H, W1, device=dev)
             for it in range(a.iters):
                 rcorr.lookup_backward(grads, coords[it % iters], go, L, r)
+            for _ in range(2):             # rc::volume_bwd_kernel (fp32 MFMA)
+                rcorr.build_backward(f1, f2, grads)
         if a.dev_variants:
             from raft_stereo_amd import _lib
             with _lib.dev_library():
