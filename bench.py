@@ -354,6 +354,8 @@ def main():
                     help="also time the whole network this many steps (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    ap.add_argument("--mfma", default=os.path.join(ROOT, "profiles", "mfma.json"),
+                    help="PMC MFMA-busy fractions per kernel (written by tools/pmc_sq.py)")
     ap.add_argument("--no-backward", action="store_true",
                     help="skip the corr-path backward timing (sceneflow only)")
     args = ap.parse_args()
@@ -525,6 +527,13 @@ def main():
     if ltraffic:   # the HBM bytes the kernel really moves (PMC), per second
         roof_lookup["traffic_gbs"] = ltraffic / (lookup_launch_ms * 1e-3) / 1e9
         roof_lookup["traffic_frac"] = roof_lookup["traffic_gbs"] / HBM_PEAK_GBS
+    mfma_pmc = load_traffic(args.mfma).get("kernels", {})
+
+    def pmc_util(prefix):
+        hit = [v for k, v in mfma_pmc.items() if prefix in k]
+        return hit[0]["mfma_util"] if hit else None
+    if not bf16:
+        roof_volume["mfma_util_pmc"] = pmc_util("build_f32_ring_kernel")
     dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
 
     result = {
@@ -566,6 +575,7 @@ def main():
             rl["traffic"] = lbt
             rl["traffic_gbs"] = lbt / (result["backward"]["lookup_bwd_us"] * 1e-6) / 1e9
             rl["traffic_frac"] = rl["traffic_gbs"] / HBM_PEAK_GBS
+        result["backward"]["roofline_volume_bwd"]["mfma_util_pmc"] = pmc_util("volume_bwd_kernel")
         result["upsample"] = upsample_timing(cfg, device)
     if args.e2e_steps > 0 and args.config == "sceneflow":
         result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1, world=world)

@@ -53,7 +53,7 @@ if has pmc; then
         --output-format csv -d "$OUT/pmc_sq" -o s -- python3 tools/probe.py
     python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --out "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
     cat "$OUT/traffic.log"
-    python tools/pmc_sq.py "$OUT/pmc_sq" > "$OUT/pmc_sq.txt" 2>&1; cat "$OUT/pmc_sq.txt"
+    python tools/pmc_sq.py "$OUT/pmc_sq" "$OUT/mfma.json" > "$OUT/pmc_sq.txt" 2>&1; cat "$OUT/pmc_sq.txt"
 fi
 if has pmcsq; then
     step pmc_sq2 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE \

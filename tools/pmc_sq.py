@@ -15,7 +15,7 @@ from collections import defaultdict
 SIMDS = 256 * 4
 
 
-def main(d):
+def main(d, json_out=None):
     agg = defaultdict(lambda: defaultdict(float))
     names, times = {}, {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -27,6 +27,7 @@ def main(d):
     per = defaultdict(list)
     for k in sorted(agg):
         per[names[k]].append((agg[k], times[k]))
+    util = {}
     for name, rows in per.items():
         n = len(rows)
         c = {key: sum(r[0].get(key, 0.0) for r in rows) / n for key in rows[0][0]}
@@ -36,7 +37,10 @@ def main(d):
         if gui and t:
             line += f" clk={gui / t / 1e9:5.2f}GHz"
             if c.get("SQ_VALU_MFMA_BUSY_CYCLES"):
-                line += f" mfma_util={c['SQ_VALU_MFMA_BUSY_CYCLES'] / (SIMDS * gui):.3f}"
+                u = c['SQ_VALU_MFMA_BUSY_CYCLES'] / (SIMDS * gui)
+                line += f" mfma_util={u:.3f}"
+                util[name] = {"mfma_util": u, "clock_ghz": gui / t / 1e9, "us": t * 1e6,
+                              "dispatches": n}
         wc = c.get("SQ_WAVE_CYCLES", 0.0)
         if wc:
             line += (f" wait={c.get('SQ_WAIT_ANY', 0) / wc:.2f} wait_inst={c.get('SQ_WAIT_INST_ANY', 0) / wc:.2f}"
@@ -46,5 +50,13 @@ def main(d):
         print(line)
 
 
+    if json_out:
+        import json
+        with open(json_out, "w") as fh:
+            json.dump({"note": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8), "
+                               "rocprofv3 --pmc pass over tools/probe.py", "kernels": util},
+                      fh, indent=1)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
