@@ -112,12 +112,16 @@ int rc_corr_lookup_conv(const void *const *pyr, const int *widths, const long *p
 
 /* Lookup over a pool-chain fp32 pyramid (what rc_corr_build writes), same
  * arguments and bit-identical results as rc_corr_lookup with RC_F32, but
- * levels >= 2 are recomputed from level 1 (level l+1 = pairwise mean of level
- * l, the fp32 ops of model.py:294), so only levels 0 and 1 are read: one
- * level-1 span per pixel instead of one window per level.  Requires
- * widths[i] == widths[i-1] / 2, pyr_ld[1] % 4 == 0, levels 3..4, radius
- * 1..4.  pyr[i >= 2] are not read (the values must still be the pool chain
- * for the results to equal rc_corr_lookup's). */
+ * some levels are recomputed from others (level l+1 = pairwise mean of level
+ * l, the fp32 ops of model.py:294) instead of read.  pyr[i], i >= 1, may be
+ * NULL (not stored); the kernel is chosen from what is given:
+ *   levels 2, or levels 4 with pyr[2] != NULL: the pair kernel reads levels 0
+ *     and 2 (one span of each serves two levels); level-0 width <= 65536;
+ *   otherwise levels 3..4 with pyr[1] != NULL: the level-1 chain kernel reads
+ *     levels 0 and 1 (one level-1 span serves levels 1..L-1).
+ * Requires widths[i] == widths[i-1] / 2, the read levels' row strides % 4 == 0,
+ * radius 1..4.  Levels given but not read must still hold the pool chain for
+ * the results to equal rc_corr_lookup's. */
 int rc_corr_lookup_chain(const void *const *pyr, const int *widths, const long *pyr_ld,
                          int levels, int radius, const float *coords_x,
                          long coord_batch_stride, int B, int H, int W1, float *out,
@@ -148,7 +152,12 @@ int rc_corr_lookup_step(const void *const *pyr, const int *widths, const long *p
  *          multiples of 4), 16-byte aligned.  Accumulates: zero the buffers
  *          once, then call once per lookup call.
  *   grad_out: [B][levels*(2r+1)][H][W1] fp32 contiguous.  Other arguments as
- *          rc_corr_lookup.  No atomics: pixel p owns row p. */
+ *          rc_corr_lookup.  No atomics: pixel p owns row p.
+ *   Pair layout: with levels 2 or 4, grad_pyr[1] (and grad_pyr[3]) NULL and
+ *          radius <= 4, the gradients of levels 1 and 3 are added, already
+ *          through avg_pool2d's backward (/2 to both children), to levels 0
+ *          and 2; pass such buffers to rc_corr_build_backward with levels = 3
+ *          and grad_pyr[1] = NULL. */
 int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long *grad_ld,
                             int levels, int radius, const float *coords_x,
                             long coord_batch_stride, int B, int H, int W1,
@@ -161,7 +170,9 @@ int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long
  *   grad_fmap2[b][d][h][w2] = sum_w1 G[b,h,w1,w2] * fmap1[b][d][h][w1]
  *   (overwritten, fp32, exact-fp32 MFMA).  grad_pyr[l], l < levels: fp32
  *   B*H*W1 rows of W2 >> l, row stride grad_ld[l] (grad_ld[0] % 4 == 0).
- *   fmap_dtype RC_F32 only.  When B*H*W1 == 0 nothing is written. */
+ *   fmap_dtype RC_F32 only.  When B*H*W1 == 0 nothing is written.
+ *   levels == 3 with grad_pyr[1] == NULL: pair-folded gradients from
+ *   rc_corr_lookup_backward's pair layout, Dl_0[k] = g_0[k] + g_2[k>>2] / 4. */
 int rc_corr_build_backward(const void *fmap1, const void *fmap2, int fmap_dtype,
                            int B, int D, int H, int W1, int W2,
                            const void *const *grad_pyr, const long *grad_ld, int levels,

@@ -278,14 +278,23 @@ def lookup_chain(pyramid, coords, num_levels, radius):
 
 # ----------------------------------------------------------------- backward
 
-def grad_buffers(P, widths, device):
+def grad_buffers(P, widths, device, pair=False):
     """Zeroed fp32 level-gradient buffers (P, W_l) with rows padded to 16 bytes
-    (the padding stays zero: rc_corr_lookup_backward never touches it)."""
+    (the padding stays zero: rc_corr_lookup_backward never touches it).
+    ``pair``: the pair layout -- levels 1 and 3 are None, their gradients are
+    folded into levels 0 and 2 by the pair backward kernel."""
     bufs = []
-    for W in widths:
+    for l, W in enumerate(widths):
+        if pair and l % 2 == 1:
+            bufs.append(None)
+            continue
         ld = -(-W // 4) * 4
         bufs.append(torch.zeros((P, ld), dtype=torch.float32, device=device)[:, :W])
     return bufs
+
+
+def _pair_grads_ok(num_levels, radius, W0):
+    return num_levels in (2, 4) and 1 <= radius <= 4 and W0 <= 65536
 
 
 def lookup_backward(grads, coords, grad_out, num_levels, radius):
@@ -299,11 +308,13 @@ def lookup_backward(grads, coords, grad_out, num_levels, radius):
     go = grad_out.detach().float().contiguous()
     if go.shape != (B, num_levels * (2 * radius + 1), H, W1):
         raise RuntimeError(f"lookup_backward: grad_out shape {tuple(go.shape)}")
+    W0 = grads[0].shape[-1]
+    g = [grads[i] for i in range(num_levels)]
     with torch.cuda.device(coords.device):
         rc = _lib.lib().rc_corr_lookup_backward(
-            _lib.ptr_array([grads[i].data_ptr() for i in range(num_levels)]),
-            _lib.int_array([grads[i].shape[-1] for i in range(num_levels)]),
-            _lib.long_array([grads[i].stride(0) for i in range(num_levels)]),
+            _lib.ptr_array([None if t is None else t.data_ptr() for t in g]),
+            _lib.int_array([W0 >> i for i in range(num_levels)]),
+            _lib.long_array([W0 >> i if t is None else t.stride(0) for i, t in enumerate(g)]),
             num_levels, radius, x.data_ptr(), cbs, B, H, W1, go.data_ptr(),
             _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup_backward")
@@ -320,12 +331,15 @@ def build_backward(fmap1, fmap2, grads):
     if B * H * W1 == 0:
         return torch.zeros_like(f1), torch.zeros_like(f2)
     df1, df2 = torch.empty_like(f1), torch.empty_like(f2)
+    # pair layout [g0, None, g2, None] -> levels 0-2 with level 1 NULL; [g0, None] -> level 0
+    if len(grads) > 1 and grads[1] is None:
+        grads = [grads[0], None, grads[2]] if len(grads) > 2 else [grads[0]]
     with torch.cuda.device(f1.device):
         rc = _lib.lib().rc_corr_build_backward(
             f1.data_ptr(), f2.data_ptr(), _lib.RC_F32, B, D, H, W1, W2,
-            _lib.ptr_array([g.data_ptr() for g in grads]),
-            _lib.long_array([g.stride(0) for g in grads]), len(grads),
-            df1.data_ptr(), df2.data_ptr(), _stream(f1.device))
+            _lib.ptr_array([None if g is None else g.data_ptr() for g in grads]),
+            _lib.long_array([W2 >> l if g is None else g.stride(0) for l, g in enumerate(grads)]),
+            len(grads), df1.data_ptr(), df2.data_ptr(), _stream(f1.device))
     _lib.check(rc, "rc_corr_build_backward")
     return df1, df2
 
@@ -338,11 +352,12 @@ class _GradState:
     def __init__(self, P, widths, device, num_levels, radius):
         self.P, self.widths, self.device = P, widths, device
         self.num_levels, self.radius = num_levels, radius
+        self.pair = _pair_grads_ok(num_levels, radius, widths[0])
         self.grads = None
 
     def accumulate(self, coords, grad_out):
         if self.grads is None:
-            self.grads = grad_buffers(self.P, self.widths, self.device)
+            self.grads = grad_buffers(self.P, self.widths, self.device, pair=self.pair)
         lookup_backward(self.grads, coords, grad_out, self.num_levels, self.radius)
 
     def take(self):

@@ -277,6 +277,194 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// lookup_bwd_pair_kernel -- the lookup backward for pool-chain gradients
+// stored as levels 0 and 2 only (the forward's pair kernel in reverse,
+// lookup.hip).  A level-(2k+1) tap contribution c to element j equals c/2 to
+// level-2k elements 2j and 2j+1 (avg_pool2d's backward, model.py:294, exact
+// in fp32), so the lane accumulates both levels of a pair into ONE register
+// window over the level-2k span [2(m-R-1), 2(m+R+3)) and read-modify-writes
+// the 16-B chunks of that span it touched: two spans per pixel instead of
+// four windows (~3.8 instead of ~5.4 64-B requests each way at the bench
+// coordinates).  rc_corr_build_backward then folds level 2
+// into level 0 (volume_bwd_kernel<.., kPairFold, ..>).  The summation order
+// differs from the per-level kernels (tolerance-level parity, not bitwise).
+// Taps never leave the window for W <= 2^16 (the argument in lookup.hip,
+// window_taps); a lane whose pair breaks n = 2m + dd (only a subnormal x)
+// updates memory tap by tap and stores no chunk.
+template <int R>
+struct PairGradSpan {
+    static constexpr int NW = 2 * R + 4, NS = 2 * NW, NC = (NS + 2 + 3) / 4;
+    f32x4 q[NC];
+    float gv[2][2 * R + 1];        // output gradients of the even / odd level
+    float m, n;
+    int sh, lo_e, hi_e;            // chunk shift; touched element range
+    bool inwin, valid;
+};
+
+template <int R>
+__device__ __forceinline__ void tap_range(float xl, int W, int &f, int &l) {
+    const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+    const DivRN dv = div_prep(Wm1);
+    const float pa = ((div_rn(2.0f * ((float)(-R) + xl), dv) - 1.0f) + 1.0f) * half;
+    const float pb = ((div_rn(2.0f * ((float)R + xl), dv) - 1.0f) + 1.0f) * half;
+    f = max((int)floorf(pa), 0);
+    l = min((int)floorf(pb) + 1, W - 1);
+}
+
+template <int R>
+__device__ __forceinline__ void issue_pair_grad(PairGradSpan<R> &ps, const LookupBwdArgs &a, int lo,
+                                                float x, const float *go, long long pblk,
+                                                long long lrow) {
+    typedef PairGradSpan<R> PS;
+    constexpr int T = 2 * R + 1;
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int t = 0; t < T; ++t) ps.gv[e][t] = go[(long long)((lo + e) * T + t) * a.HW];
+    const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+    const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+    ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));   // false for NaN
+    ps.m = ps.inwin ? floorf(xhi) : 0.0f;
+    ps.n = ps.inwin ? floorf(xlo) : 0.0f;
+    const int dd = (int)ps.n - 2 * (int)ps.m;
+    ps.valid = ps.inwin && (dd == 0 || dd == 1);
+    ps.lo_e = 0x7FFFFFFF;
+    ps.hi_e = -1;
+    if (ps.valid) {
+        int f, l;
+        tap_range<R>(xlo, Wlo, f, l);
+        if (f <= l) { ps.lo_e = f; ps.hi_e = l; }
+        tap_range<R>(xhi, Whi, f, l);
+        if (f <= l) { ps.lo_e = min(ps.lo_e, 2 * f); ps.hi_e = max(ps.hi_e, 2 * l + 1); }
+    }
+    const int sa = 2 * ((int)ps.m - R - 1), ea = sa & ~3;
+    ps.sh = sa - ea;
+    const long long ld = a.ld[lo];
+    const auto rs = make_rsrc(a.g[lo] + pblk * ld, clamp_bytes((a.P - pblk) * ld * 4));
+#pragma unroll
+    for (int k = 0; k < PS::NC; ++k) {
+        const int cs = ea + 4 * k;
+        const bool ok = cs <= ps.hi_e && cs + 3 >= ps.lo_e;   // inside the row (lo_e >= 0, hi_e < W)
+        ps.q[k] = ld4(rs, ok ? (uint32_t)((lrow * ld + cs) * 4) : 0xFFFFFF00u);
+    }
+}
+
+// acc[j] += v at the runtime index j = base + STRIDE*off, off in [0, NOFF),
+// with static indices only (the window stays in registers).
+template <int NS, int NOFF, int STRIDE = 1>
+__device__ __forceinline__ void win_add(float (&acc)[NS], int base, int off, float v) {
+#pragma unroll
+    for (int q = 0; q < NOFF; ++q) {
+        const int j = base + STRIDE * q;
+        if (j >= 0 && j < NS) acc[j] += (off == q) ? v : 0.0f;
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void finish_pair_grad(PairGradSpan<R> &ps, const LookupBwdArgs &a, int lo,
+                                                 float x, long long p) {
+    typedef PairGradSpan<R> PS;
+    constexpr int T = 2 * R + 1, NS = PS::NS;
+    const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+    const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+    float *row = a.g[lo] + p * a.ld[lo];
+    if (__builtin_expect(ps.inwin && !ps.valid, 0)) {   // subnormal x: tap by tap, to memory
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int W = e ? Whi : Wlo;
+            const float xl = e ? xhi : xlo, Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+            const DivRN dv = div_prep(Wm1);
+            for (int t = 0; t < T; ++t) {
+                const float xp = ((div_rn(2.0f * ((float)(t - R) + xl), dv) - 1.0f) + 1.0f) * half;
+                const float x0 = floorf(xp);
+                const float c1 = (xp - x0) * ps.gv[e][t], c0 = ((x0 + 1.0f) - xp) * ps.gv[e][t];
+                for (int s = 0; s < 2; ++s) {
+                    const float xe = x0 + (float)s;
+                    if (!(xe >= 0.0f && xe <= Wm1)) continue;
+                    const float c = s ? c1 : c0;
+                    if (e == 0) row[(long long)xe] += c;
+                    else { row[2 * (long long)xe] += c * 0.5f; row[2 * (long long)xe + 1] += c * 0.5f; }
+                }
+            }
+        }
+        return;
+    }
+    if (ps.hi_e < ps.lo_e) return;                       // nothing in range (or !inwin)
+    // register window over the span: acc[j] <-> element 2(m-R-1) + j
+    float acc[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) acc[j] = 0.0f;
+    const int dd = (int)ps.n - 2 * (int)ps.m;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int W = e ? Whi : Wlo;
+        const float xl = e ? xhi : xlo, nwin = e ? ps.m : ps.n;
+        const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+        const DivRN dv = div_prep(Wm1);
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + xl;
+            const float xn = div_rn(2.0f * xt, dv) - 1.0f;        // model.py:271
+            const float xp = (xn + 1.0f) * half;               // :275 unnormalise
+            const float x0 = floorf(xp);
+            const float w1 = xp - x0, w0 = (x0 + 1.0f) - xp;   // ne / nw corner weights
+            const float gv = ps.gv[e][t];
+            const float c0 = w0 * gv, c1 = w1 * gv;
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            const float nt = nwin + (float)(t - R);
+            const int d = x0 < nt ? 0 : (x0 > nt ? 2 : 1);     // window index of x0 is t + d
+            if (e == 0) {
+                // even level: element n-R-1+(t+d) is span index dd+R+1+t+d
+                win_add<NS, 4>(acc, R + 1 + t, dd + d, ok0 ? c0 : 0.0f);
+                win_add<NS, 4>(acc, R + 2 + t, dd + d, ok1 ? c1 : 0.0f);
+            } else {
+                // odd level: element m-R-1+(t+d) covers span indices 2(t+d), 2(t+d)+1
+                const float h0 = ok0 ? c0 * 0.5f : 0.0f, h1 = ok1 ? c1 * 0.5f : 0.0f;
+                win_add<NS, 3, 2>(acc, 2 * t, d, h0);
+                win_add<NS, 3, 2>(acc, 2 * t + 1, d, h0);
+                win_add<NS, 3, 2>(acc, 2 * t + 2, d, h1);
+                win_add<NS, 3, 2>(acc, 2 * t + 3, d, h1);
+            }
+        }
+    }
+    // read-modify-write the touched chunks: chunk k = elements ea+4k.., span
+    // index 4k+c-sh (sh in {0, 2})
+    const int ea = 2 * ((int)ps.m - R - 1) - ps.sh;
+#pragma unroll
+    for (int k = 0; k < PS::NC; ++k) {
+        const int cs = ea + 4 * k;
+        if (cs > ps.hi_e || cs + 3 < ps.lo_e) continue;
+        f32x4 w = ps.q[k];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int j0 = 4 * k + c, j2 = 4 * k + c - 2;
+            const float a0 = j0 < NS ? acc[j0] : 0.0f;
+            const float a2 = (j2 >= 0 && j2 < NS) ? acc[j2] : 0.0f;
+            w[c] += ps.sh ? a2 : a0;
+        }
+        *reinterpret_cast<f32x4 *>(row + cs) = w;
+    }
+}
+
+// NL = 2 (levels 0-1) or 4 (levels 0-3); a.g[1] (and a.g[3]) are not used.
+template <int R, int NL>
+__global__ __launch_bounds__(256) void lookup_bwd_pair_kernel(LookupBwdArgs a) {
+    static_assert(NL == 2 || NL == 4, "pair backward: 2 or 4 levels");
+    constexpr int NP = NL / 2, T = 2 * R + 1;
+    const long long pblk = (long long)blockIdx.x * 256;
+    const long long p = pblk + threadIdx.x;
+    if (p >= a.P) return;   // no barriers in this kernel
+    const long long bimg = p / a.HW, rem = p - bimg * a.HW;
+    const float x = a.coords[bimg * a.cbs + rem];
+    const float *go = a.grad_out + bimg * (long long)(NL * T) * a.HW + rem;
+    PairGradSpan<R> sp[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) issue_pair_grad<R>(sp[k], a, 2 * k, x, go, pblk, p - pblk);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) finish_pair_grad<R>(sp[k], a, 2 * k, x, p);
+}
+
 // ---------------------------------------------------------------- volume bwd
 
 // Reduction elements per stage KS = 32 (LDS rows of 40 floats) or 16 (rows
@@ -291,10 +479,15 @@ struct BwdTile {
 
 // Raw level-gradient values behind G[w1][w2 .. w2+3] (w2 % 4 == 0): loaded
 // in one stage, folded in the next (so the loads overlap the MFMAs).
-// NLEV = the exact level count (1..4, compile time) or 0 (any, up to 8).
+// NLEV = the exact level count (1..4, compile time), 0 (any, up to 8), or
+// kPairFold: gradients of levels 0 and 2 only, levels 1 and 3 already folded
+// into them by lookup_bwd_pair_kernel (g[1] = g[3] = NULL, nlev = 3):
+//   Dl_0[k] = g0[k] + ((g2[k>>2] * 0.5) * 0.5),  k>>2 < W_2
+// (the generic fold with a zero level 1, in the same fp32 operations).
+constexpr int kPairFold = -1;
 template <int NLEV>
 struct FoldRaw {
-    static constexpr int NC = NLEV == 0 ? kMaxLevels - 2 : (NLEV > 2 ? NLEV - 2 : 0);
+    static constexpr int NC = NLEV == kPairFold ? 1 : NLEV == 0 ? kMaxLevels - 2 : (NLEV > 2 ? NLEV - 2 : 0);
     f32x4 g0;
     float l1[2];                   // level 1 at w2/2, w2/2 + 1
     float lc[NC > 0 ? NC : 1];     // level i >= 2 at w2 >> i (one value per quad)
@@ -311,6 +504,11 @@ __device__ __forceinline__ void fold_load(const BuildBwdArgs &a, long long prow,
     if (!ok || w2 >= a.W2) return;
     // rows of level 0 are padded to a multiple of 4, so the quad is in the row
     r.g0 = *reinterpret_cast<const f32x4 *>(a.g[0] + prow * a.ld[0] + w2);
+    if constexpr (NLEV == kPairFold) {      // one level-2 value per quad
+        const int k = w2 >> 2;
+        if (k < a.Wl[2]) r.lc[0] = a.g[2][prow * a.ld[2] + k];
+        return;
+    }
     if (NLEV >= 2 || (NLEV == 0 && a.nlev > 1)) {
         const int k = w2 >> 1;
         const float *g1 = a.g[1] + prow * a.ld[1];
@@ -328,6 +526,16 @@ template <int NLEV>
 __device__ __forceinline__ f32x4 fold_math(const BuildBwdArgs &a, int w2, const FoldRaw<NLEV> &r) {
     constexpr int NC = FoldRaw<NLEV>::NC;
     f32x4 out;
+    if constexpr (NLEV == kPairFold) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float t = (((w2 + c) >> 2) < a.Wl[2]) ? (r.lc[0] * 0.5f) * 0.5f : 0.0f;
+            float d0 = r.g0[c] + t;
+            d0 = (w2 + c < a.W2) ? d0 : 0.0f;
+            out[c] = a.pow2 ? d0 * a.scale : d0 / a.sq;
+        }
+        return out;
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         float t = 0.0f;   // Dl_i, i from nlev-1 down to 1
@@ -360,6 +568,7 @@ __device__ __forceinline__ f32x4 load_x_quad(const float *rowp, int k, int K, bo
 template <bool VEC, int NLEV, int KS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NLEV == 0 ? 1 : 2)))
 void volume_bwd_kernel(BuildBwdArgs a, int nwg_total) {
+    static_assert(NLEV >= kPairFold, "level count");
     typedef BwdTile<KS> TL;
     constexpr int kBwdK = KS, kBwdRow = TL::ROW, QPT = TL::QPT;
     __shared__ __attribute__((aligned(16))) float smem[2][2][TL::IMG];   // [buf][X | Y]
@@ -489,6 +698,20 @@ void volume_bwd_kernel(BuildBwdArgs a, int nwg_total) {
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    if (a.levels >= 2 && a.g[1] == nullptr) {   // pair-folded gradient buffers (levels 0, 2)
+#define RC_LBWDP(RR)                                                                                 \
+    if (a.levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<RR, 4>), dim3(nblk), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<RR, 2>), dim3(nblk), dim3(256), 0, s, a);
+        switch (radius) {
+            case 1: RC_LBWDP(1) break;
+            case 2: RC_LBWDP(2) break;
+            case 3: RC_LBWDP(3) break;
+            case 4: RC_LBWDP(4) break;
+            default: return hipErrorInvalidValue;
+        }
+#undef RC_LBWDP
+        return hipGetLastError();
+    }
 #ifdef RAFTCORR_DEV
     // dev library A/B: RAFTCORR_LOOKUP_BWD_VARIANT=1 forces the per-level-wait kernel
     const int variant = rc::dev_knob("RAFTCORR_LOOKUP_BWD_VARIANT");
@@ -550,6 +773,11 @@ hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s) {
                                 grid, blk, 0, s, a, (int)nwg);                                      \
     else hipLaunchKernelGGL((rc::volume_bwd_kernel<false, NL, (NL == 1 || NL == 2) ? 32 : 16>),     \
                             grid, blk, 0, s, a, (int)nwg);
+    if (a.nlev == 3 && a.g[1] == nullptr) {   // pair-folded gradients (levels 0 and 2)
+        if (vec) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, rc::kPairFold, 32>), grid, blk, 0, s, a, (int)nwg);
+        else hipLaunchKernelGGL((rc::volume_bwd_kernel<false, rc::kPairFold, 32>), grid, blk, 0, s, a, (int)nwg);
+        return hipGetLastError();
+    }
     switch (a.nlev) {   // the level count fixes the fold's loads at compile time
         case 1: RC_VBWD(1) break;
         case 2: RC_VBWD(2) break;

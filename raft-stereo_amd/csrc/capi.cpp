@@ -304,10 +304,31 @@ extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
     rc::LookupArgs la;
     bool empty;
     int rc = prep_lookup("rc_corr_lookup_backward", grad_pyr, widths, grad_ld, RC_F32, levels,
-                         radius, coords_x, coord_batch_stride, B, H, W1, grad_out, la, &empty);
+                         radius, coords_x, coord_batch_stride, B, H, W1, grad_out, la, &empty, true);
     if (rc || empty) return rc;
+    // pair-folded buffers: levels 1 and 3 NULL, their gradients folded into
+    // levels 0 and 2 (2 or 4 levels, radius 1..4, widths halving, W <= 2^16)
+    const bool pair = levels >= 2 && !grad_pyr[1];
+    if (pair) {
+        bool ok = (levels == 2 || (levels == 4 && grad_pyr[2] && !grad_pyr[3])) && radius <= 4 &&
+                  widths[0] <= 65536;
+        for (int i = 1; i < levels; ++i) ok = ok && widths[i] == widths[i - 1] / 2;
+        if (!ok)
+            return fail(RC_EINVAL, "rc_corr_lookup_backward: NULL gradient levels need the pair "
+                        "layout (levels 2 or 4, level 1 [and 3] NULL, radius <= 4, halving widths)");
+    } else {
+        for (int i = 1; i < levels; ++i)
+            if (!grad_pyr[i])
+                return fail(RC_EINVAL, "rc_corr_lookup_backward: level %d null", i);
+    }
     rc::LookupBwdArgs a{};
     for (int i = 0; i < levels; ++i) {
+        if (!grad_pyr[i]) {
+            a.g[i] = nullptr;
+            a.W[i] = la.W[i];
+            a.ld[i] = la.ld[i];
+            continue;
+        }
         if (la.ld[i] % 4 != 0)
             return fail(RC_EINVAL, "rc_corr_lookup_backward: row stride %lld of level %d is not a "
                         "multiple of 4", la.ld[i], i);
@@ -344,8 +365,16 @@ extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int 
         return fail(RC_EINVAL, "rc_corr_build_backward: feature maps and their gradients must be "
                     "non-null and 16-byte aligned");
     rc::BuildBwdArgs a{};
+    // levels == 3 with grad_pyr[1] NULL: pair-folded gradients (levels 0, 2)
+    const bool pair = levels == 3 && !grad_pyr[1];
     for (int l = 0; l < levels; ++l) {
         const long ld = grad_ld ? grad_ld[l] : (long)(W2 >> l);
+        if (pair && l == 1) {
+            a.g[1] = nullptr;
+            a.ld[1] = W2 >> 1;
+            a.Wl[1] = W2 >> 1;
+            continue;
+        }
         if (!grad_pyr[l] || !aligned16(grad_pyr[l]))
             return fail(RC_EINVAL, "rc_corr_build_backward: level gradient %d null or not 16-byte "
                         "aligned", l);

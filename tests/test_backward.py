@@ -219,3 +219,55 @@ def test_backward_bf16_fmaps_and_unused_lookup():
     with torch.no_grad():
         out = CorrBlock1D(h1, h1, num_levels=2, radius=2)(c)
     assert out.grad_fn is None
+
+
+PAIR_SHAPES = [
+    # B, D, H, W1, W2, L, r, calls
+    (2, 32, 3, 57, 240, 4, 4, 3),
+    (1, 16, 2, 40, 311, 4, 3, 2),      # odd widths 311/155/77/38
+    (1, 8, 2, 33, 64, 2, 2, 3),        # 2 levels: level 1 folded into level 0
+    (1, 8, 2, 20, 16, 4, 1, 2),        # level 3 of width 2
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", PAIR_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_pair_layout_backward(shape):
+    """The pair layout (levels 1, 3 folded into 0, 2 by lookup_bwd_pair_kernel,
+    then rc_corr_build_backward's pair fold) vs the oracle's per-level
+    gradients folded the same way (<= 1e-6 normalised: only the order of
+    additions differs), and its fmap gradients vs the per-level layout's
+    (fp32 contract), NaN / inf / far out-of-range coords included."""
+    from raft_stereo_amd import corr as rcorr
+    B, D, H, W1, W2, L, r, calls = shape
+    g = torch.Generator().manual_seed(sum(shape) * 7)
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    widths = [W2 >> i for i in range(L)]
+    cs, gs = [], []
+    for _ in range(calls):
+        x = torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 48
+        x[..., ::5] = torch.randint(-20, W2 + 20, x[..., ::5].shape, generator=g).float()
+        x[0, 0, 0, :6] = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e30, -1e30, 0.5])
+        cs.append(torch.cat([x, torch.randn(B, 1, H, W1, generator=g)], 1))
+        gs.append(torch.randn(B, L * (2 * r + 1), H, W1, generator=g))
+    P = B * H * W1
+    pair = rcorr.grad_buffers(P, widths, torch.device(DEV), pair=True)
+    full = rcorr.grad_buffers(P, widths, torch.device(DEV))
+    for c, go in zip(cs, gs):
+        rcorr.lookup_backward(pair, c.to(DEV), go.to(DEV), L, r)
+        rcorr.lookup_backward(full, c.to(DEV), go.to(DEV), L, r)
+    ref = None
+    for c, go in zip(cs, gs):
+        ref = coracle.corr_lookup_backward(widths, c.numpy(), go.numpy(), L, r, ref)
+    for e in range(0, L, 2):                 # ref_e = g_e + avg_pool2d backward of g_{e+1}
+        want = np.array(ref[e], dtype=np.float64)
+        half = np.repeat(np.asarray(ref[e + 1], np.float64) * 0.5, 2, axis=1)
+        want[:, :half.shape[1]] += half
+        got = pair[e].cpu().numpy()
+        assert norm_err(got, want) <= 1e-6, f"level {e}"
+    a1, a2 = rcorr.build_backward(f1.to(DEV), f2.to(DEV), pair)
+    b1, b2 = rcorr.build_backward(f1.to(DEV), f2.to(DEV), full)
+    for a_, b_ in ((a1, b1), (a2, b2)):
+        a_, b_ = a_.cpu().numpy(), b_.cpu().numpy()
+        assert norm_err(a_, b_) <= 1e-5 and rel_l2(a_, b_) <= 1e-6
