@@ -247,7 +247,8 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
     widths = [W2 >> i for i in range(L)]
     g = torch.Generator().manual_seed(99)
     gouts = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(2)]
-    grads = rcorr.grad_buffers(P, widths, dev)
+    pair = rcorr._pair_grads_ok(L, r, W2)      # the layout CorrBlock1D's autograd uses
+    grads = rcorr.grad_buffers(P, widths, dev, pair=pair)
 
     def lbwd(c, go):
         rcorr.lookup_backward(grads, c, go, L, r)
@@ -286,18 +287,22 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
     torch.cuda.synchronize()
     step_ms = (time.perf_counter() - t0) / reps * 1e3
     vflops = 2 * volume_flops(B, D, H, W1, W2)        # two GEMMs
-    lbytes = P * (4 + L * (2 * r + 1) * 4 + 2 * L * (2 * r + 2) * 4)   # x, grad_out, window RMW
+    # x, grad_out, per-level window RMW (the layout-independent definition of
+    # round 1; the pair layout's RMW touches 2 spans of 2(2r+4) elements instead)
+    lbytes = P * (4 + L * (2 * r + 1) * 4 + 2 * L * (2 * r + 2) * 4)
     return {"lookup_bwd_us": lb_ms * 1e3, "volume_bwd_us": vb_ms * 1e3,
             "train_step_ms": step_ms, "train_pairs_per_s": B / (step_ms * 1e-3),
             "roofline_volume_bwd": {"bound": "mfma", "achieved": vflops / (vb_ms * 1e-3) / 1e12,
                                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                     "frac": vflops / (vb_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                                    "kernel": f"rc::volume_bwd_kernel<true,{L}>"},
+                                    "kernel": ("rc::volume_bwd_kernel<true,kPairFold>" if pair
+                                               else f"rc::volume_bwd_kernel<true,{L}>")},
             "roofline_lookup_bwd": {"bound": "hbm", "achieved": lbytes / (lb_ms * 1e-3) / 1e9,
                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": lbytes / (lb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                     "algorithmic_bytes": lbytes,
-                                    "kernel": (f"rc::lookup_bwd_pre_kernel<{r},{L}>" if r <= 4 and L <= 4
+                                    "kernel": (f"rc::lookup_bwd_pair_kernel<{r},{L}>" if pair else
+                                               f"rc::lookup_bwd_pre_kernel<{r},{L}>" if r <= 4 and L <= 4
                                                else f"rc::lookup_bwd_kernel<{r}>")},
             "note": "step = CorrBlock1D build + lookups + autograd backward to both fmaps "
                     "(random output gradients); kernel times are medians of event-timed launches"}
@@ -330,6 +335,11 @@ def upsample_timing(cfg, device, reps=20):
                          "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "kernel": "rc::convex_upsample_kernel<4>"},
             "shape": {"flow": [B, 1, H, W1], "mask": [B, 9 * f * f, H, W1], "factor": f}}
+
+
+def rcorr_pair(L, r, W2):
+    from raft_stereo_amd import corr as rcorr
+    return rcorr._pair_grads_ok(L, r, W2)
 
 
 def load_traffic(path):
@@ -569,7 +579,7 @@ def main():
     }
     if not args.no_backward and args.config == "sceneflow":
         result["backward"] = backward_timing(cfg, f1, f2, coords)
-        lbt = traffic.get("lookup_bwd_bytes")
+        lbt = traffic.get("lookup_bwd_pair_bytes" if rcorr_pair(L, r, W2) else "lookup_bwd_bytes")
         if lbt:   # PMC bytes the lookup backward really moves, per launch
             rl = result["backward"]["roofline_lookup_bwd"]
             rl["traffic"] = lbt

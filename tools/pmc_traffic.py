@@ -57,7 +57,8 @@ def main():
     res = {}
     for kname, key in (("build", "build_"), ("lookup", "lookup_kernel"),
                        ("lookup_chain", "lookup_chain_kernel"), ("lookup_pair", "lookup_pair_kernel"),
-                       ("lookup_bwd", "lookup_bwd_pre_kernel")):
+                       ("lookup_bwd", "lookup_bwd_pre_kernel"),
+                       ("lookup_bwd_pair", "lookup_bwd_pair_kernel")):
         f = per_kernel(fr, key)
         w = per_kernel(wr, key)
         if f is None or w is None:

@@ -53,12 +53,13 @@ def main():
                 rcorr.lookup_chain(lv, coords[it % iters], L, r)
         if pdt == torch.float32:           # rc::lookup_bwd_pre_kernel (one per lookup call)
             P = B * H * W1
-            grads = rcorr.grad_buffers(P, [W2 >> i for i in range(L)], dev)
             go = torch.randn(B, L * (2 * r + 1), H, W1, device=dev)
-            for it in range(a.iters):
-                rcorr.lookup_backward(grads, coords[it % iters], go, L, r)
-            for _ in range(2):             # rc::volume_bwd_kernel (fp32 MFMA)
-                rcorr.build_backward(f1, f2, grads)
+            for pair in (False, True):     # lookup_bwd_pre_kernel, lookup_bwd_pair_kernel
+                grads = rcorr.grad_buffers(P, [W2 >> i for i in range(L)], dev, pair=pair)
+                for it in range(a.iters):
+                    rcorr.lookup_backward(grads, coords[it % iters], go, L, r)
+                for _ in range(2):         # rc::volume_bwd_kernel (fp32 MFMA)
+                    rcorr.build_backward(f1, f2, grads)
         if a.dev_variants:
             from raft_stereo_amd import _lib
             with _lib.dev_library():
