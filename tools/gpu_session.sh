@@ -31,6 +31,7 @@ has probe && step line_probe 300 python tools/line_probe.py
 has lprobe && step lookup_probe 300 python tools/lookup_probe.py --dev-variants ${LPROBE_VARIANTS:-201,202}
 has gprobe && step gather_probe 300 python tools/gather_probe.py
 has timeline && step lookup_timeline 300 python tools/lookup_timeline.py
+has shard && step shard_probe 600 python tools/shard_probe.py
 has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
 has ablateb && step ablate_bwd 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --bwd
 has ablatec && step ablate_conv 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --convc1

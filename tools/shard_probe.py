@@ -1,0 +1,103 @@
+"""Config 4 (Middlebury 1984x2880, bs=1, 32 iters) on ONE GPU: the pieces of
+the row-sharded forward, timed separately, and the scaling cap they imply.
+
+    python tools/shard_probe.py [--iters 32] [--halo 32]
+
+shard.RowShardedStereo runs the encoders (cnet + conv2 + context convs,
+model.py:359-365) REPLICATED on the full image on every rank and shards only
+the per-iteration work (corr lookup + GRU update, model.py:374-383) by rows
+of the 1/4-resolution grid, each rank keeping a +-halo slab.  Timed here:
+  E    = RAFTStereo.features on the full image (every rank pays it);
+  C(n) = the corr build of an n-row slab;
+  U(n) = one iteration on an n-row slab: lookup + update block (with the
+         slab-local interp of RowShardedStereo._gru), n = H1/N + 2*halo;
+then T(N) = E + C(n_N) + iters * U(n_N) (halo exchange not included: a few
+MB per neighbour per iteration over xGMI, tens of us) and the speedup
+T(1) / T(N).  The replicated encoder bounds it: T(N) >= E.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import pkgload  # noqa: E402
+
+pkgload.load()
+from raft_stereo_amd.network import RAFTStereo, StereoArgs  # noqa: E402
+from raft_stereo_amd.shard import RowShardedStereo  # noqa: E402
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=32)
+    ap.add_argument("--halo", type=int, default=32)
+    ap.add_argument("--H", type=int, default=1984)
+    ap.add_argument("--W", type=int, default=2880)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs()).eval().to(dev)
+    g = torch.Generator().manual_seed(1234)
+    img1 = (torch.rand(1, 3, a.H, a.W, generator=g) * 255).to(dev)
+    img2 = torch.roll(img1, -8, dims=-1)
+    res = {"image": [a.H, a.W], "iters": a.iters, "halo": a.halo}
+    with torch.no_grad():
+        E = timed(lambda: model.features(img1, img2))
+        fmap1, fmap2, net, inp = model.features(img1, img2)
+        H1 = fmap1.shape[2]
+        res["E_encoders_ms"] = E * 1e3
+        blk = model.update_block
+        out = {}
+        for N in (1, 2, 4, 8):
+            rs = RowShardedStereo(model, 0, N, halo=a.halo)
+            r0, r1, e0, e1 = rs._ranges(H1)
+            # rank 0 holds [0, r1 + halo): the largest slab is a middle rank's
+            n = min(H1, (r1 - r0) + (2 * a.halo if N > 2 else a.halo if N == 2 else 0))
+            sl = lambda t, l: t[:, :, : max(1, -(-n // (1 << l)))].contiguous()
+            f1, f2 = fmap1[:, :, :n].contiguous(), fmap2[:, :, :n].contiguous()
+            C = timed(lambda: model.corr_block(f1, f2, radius=4, num_levels=4))
+            corr_fn = model.corr_block(f1, f2, radius=4, num_levels=4)
+            c1 = model.initialize_flow(sl(net[0], 0))[1]
+            nets = [sl(t, l) for l, t in enumerate(net)]
+            inps = [[sl(c, l) for c in cl] for l, cl in enumerate(inp)]
+
+            def one_iter():
+                corr = corr_fn(c1)
+                flow = c1 - c1
+                RowShardedStereo._gru(blk, list(nets), inps, corr, flow,
+                                      lambda x, ls, ld: torch.nn.functional.interpolate(
+                                          x, nets[ld].shape[2:], mode="bilinear",
+                                          align_corners=True), True, True, True)
+            U = timed(one_iter)
+            T = E + C + a.iters * U
+            out[N] = {"slab_rows": n, "C_build_ms": C * 1e3, "U_iter_ms": U * 1e3,
+                      "T_ms": T * 1e3}
+        T1 = out[1]["T_ms"]
+        for N in out:
+            out[N]["speedup"] = T1 / out[N]["T_ms"]
+            out[N]["encoder_share"] = res["E_encoders_ms"] / out[N]["T_ms"]
+        res["per_N"] = out
+        res["amdahl_cap"] = T1 / res["E_encoders_ms"]
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
