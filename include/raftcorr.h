@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 3
+#define RC_ABI_VERSION 4
 
 /* element types */
 #define RC_F32  0
@@ -119,11 +119,14 @@ int rc_corr_lookup_conv(const void *const *pyr, const int *widths, const long *p
  *     and 2 (one span of each serves two levels); level-0 width <= 65536;
  *   otherwise levels 3..4 with pyr[1] != NULL: the level-1 chain kernel reads
  *     levels 0 and 1 (one level-1 span serves levels 1..L-1).
- * Requires widths[i] == widths[i-1] / 2, the read levels' row strides % 4 == 0,
- * radius 1..4.  Levels given but not read must still hold the pool chain for
- * the results to equal rc_corr_lookup's. */
+ * Requires widths[i] == widths[i-1] / 2, the read levels' row strides whole
+ * 16-B chunks, radius 1..4.  Levels given but not read must still hold the
+ * pool chain for the results to equal rc_corr_lookup's.  pyr_dtype RC_BF16
+ * (pair layout only): every level is the bf16-rounded pool of the level below
+ * as stored -- what rc_corr_build and rc_corr_pool write for a bf16 pyramid,
+ * and what avg_pool2d gives on bf16 tensors.  (ABI v4 added pyr_dtype.) */
 int rc_corr_lookup_chain(const void *const *pyr, const int *widths, const long *pyr_ld,
-                         int levels, int radius, const float *coords_x,
+                         int pyr_dtype, int levels, int radius, const float *coords_x,
                          long coord_batch_stride, int B, int H, int W1, float *out,
                          void *stream);
 

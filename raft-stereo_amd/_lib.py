@@ -17,7 +17,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 RC_F32, RC_BF16 = 0, 1
 RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # name -> (restype, argtypes); must match include/raftcorr.h exactly.
 _vp, _i, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
@@ -32,7 +32,7 @@ SIGNATURES = {
     "rc_corr_lookup_conv": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i,
                                  _i, _i, _vp, _l, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "rc_corr_lookup_chain": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i,
-                                  _i, _vp, _l, _i, _i, _i, _vp, _vp]),
+                                  _i, _i, _vp, _l, _i, _i, _i, _vp, _vp]),
     "rc_corr_lookup_step": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l), _i,
                                  _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "rc_corr_lookup_backward": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l),

@@ -246,13 +246,14 @@ def _chain_args(pyramid, num_levels):
     lv = [None if t is None else
           (t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous())
           for t in list(pyramid[:num_levels]) + [None] * (num_levels - len(pyramid))]
-    if any(t is not None and t.dtype != torch.float32 for t in lv):
-        raise TypeError("lookup_chain: fp32 pyramid levels required")
+    dt = lv[0].dtype
+    if any(t is not None and t.dtype != dt for t in lv):
+        raise TypeError("lookup_chain: pyramid levels of one dtype required")
     W0 = lv[0].shape[-1]
     ptrs = _lib.ptr_array([None if t is None else t.data_ptr() for t in lv])
     widths = _lib.int_array([W0 >> i for i in range(num_levels)])
     lds = _lib.long_array([W0 >> i if t is None else _row_stride(t) for i, t in enumerate(lv)])
-    return lv, ptrs, widths, lds
+    return lv, ptrs, widths, lds, _dtype_code(dt)
 
 
 def lookup_chain(pyramid, coords, num_levels, radius):
@@ -267,10 +268,10 @@ def lookup_chain(pyramid, coords, num_levels, radius):
                       device=coords.device)
     if B * H * W1 == 0:
         return out
-    keep, ptrs, widths, lds = _chain_args(pyramid, num_levels)
+    keep, ptrs, widths, lds, dt = _chain_args(pyramid, num_levels)
     with torch.cuda.device(coords.device):
         rc = _lib.lib().rc_corr_lookup_chain(
-            ptrs, widths, lds, num_levels, radius, x.data_ptr(), cbs, B, H, W1,
+            ptrs, widths, lds, dt, num_levels, radius, x.data_ptr(), cbs, B, H, W1,
             out.data_ptr(), _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup_chain")
     return out
@@ -424,8 +425,10 @@ class CorrBlock1D:
         # levels are built only when ``corr_pyramid`` is read (``lazy_levels``,
         # default on in that case): same values, same shapes, pooled by the
         # same fp32 ops.
-        self._chain = (pyramid_dtype == torch.float32 and num_levels in (2, 3, 4)
-                       and 1 <= radius <= 4 and fmap2.shape[-1] <= 65536)
+        # (bf16 pyramids: the pair layout only -- 2 or 4 levels)
+        self._chain = (1 <= radius <= 4 and fmap2.shape[-1] <= 65536 and
+                       (num_levels in (2, 3, 4) if pyramid_dtype == torch.float32 else
+                        num_levels in (2, 4) if pyramid_dtype == torch.bfloat16 else False))
         lazy = self._chain if lazy_levels is None else (bool(lazy_levels) and self._chain)
         with torch.no_grad():
             if lazy and num_levels == 3:
@@ -510,8 +513,7 @@ class CorrBlock1D:
         if B * H * W1 == 0:
             return corr, new, flow
         if self._chain:
-            keep, ptrs, widths, lds = _chain_args(self._levels, L)
-            dt = _lib.RC_F32
+            keep, ptrs, widths, lds, dt = _chain_args(self._levels, L)
         else:
             keep, ptrs, widths, lds, dt = _level_args(self.corr_pyramid, L)
         with torch.cuda.device(c1.device):

@@ -214,14 +214,16 @@ int chain_kind(const char *who, const void *const *pyr, const int *widths, int l
     return RC_OK;
 }
 
-// Row strides the chain kernels read with 16-B chunks must be multiples of 4.
-int chain_strides(const char *who, const rc::LookupArgs &a, bool pair) {
+// Row strides the chain kernels read with 16-B chunks must be whole chunks
+// (multiples of 4 fp32 / 8 bf16 elements).
+int chain_strides(const char *who, const rc::LookupArgs &a, bool pair, bool bf16 = false) {
     const int need[2] = {0, pair ? 2 : 1};
+    const int epc = bf16 ? 8 : 4;
     for (int k = 0; k < 2; ++k) {
         const int i = need[k];
-        if (i < a.levels && a.ld[i] % 4 != 0)
-            return fail(RC_EINVAL, "%s: level-%d row stride %lld is not a multiple of 4", who, i,
-                        a.ld[i]);
+        if (i < a.levels && a.ld[i] % epc != 0)
+            return fail(RC_EINVAL, "%s: level-%d row stride %lld is not a multiple of %d", who, i,
+                        a.ld[i], epc);
     }
     return RC_OK;
 }
@@ -244,22 +246,26 @@ extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, const l
 }
 
 extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, const long *pyr_ld,
-                                    int levels, int radius, const float *coords_x,
+                                    int pyr_dtype, int levels, int radius, const float *coords_x,
                                     long coord_batch_stride, int B, int H, int W1, float *out,
                                     void *stream) {
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
-    int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, RC_F32, levels, radius,
+    int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty, true);
     if (rc) return rc;
     bool pair;
     if ((rc = chain_kind("rc_corr_lookup_chain", pyr, widths, levels, radius, &pair))) return rc;
+    if (pyr_dtype == RC_BF16 && !pair)
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: a bf16 pyramid needs the pair layout "
+                    "(2 levels, or 4 with level 2 given)");
     if (empty) return RC_OK;
     a.out = out;
-    if ((rc = chain_strides("rc_corr_lookup_chain", a, pair))) return rc;
+    if ((rc = chain_strides("rc_corr_lookup_chain", a, pair, pyr_dtype == RC_BF16))) return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return hip_rc(pair ? rc_launch_lookup_pair(a, radius, s) : rc_launch_lookup_chain(a, radius, s),
+    return hip_rc(pair ? rc_launch_lookup_pair(a, radius, pyr_dtype == RC_BF16, s)
+                       : rc_launch_lookup_chain(a, radius, s),
                   "rc_corr_lookup_chain: launch");
 }
 
@@ -278,10 +284,10 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
         return fail(RC_EINVAL, "rc_corr_lookup_step: null coords1_out / flow_out");
     bool pair = false;
     if (chain) {
-        if (pyr_dtype != RC_F32)
-            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: chain needs an fp32 pyramid");
         if ((rc = chain_kind("rc_corr_lookup_step", pyr, widths, levels, radius, &pair))) return rc;
-        if ((rc = chain_strides("rc_corr_lookup_step", a, pair))) return rc;
+        if (pyr_dtype != RC_F32 && !pair)
+            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: a bf16 pyramid needs the pair layout");
+        if ((rc = chain_strides("rc_corr_lookup_step", a, pair, pyr_dtype == RC_BF16))) return rc;
     }
     a.out = out;
     a.step = 1;
@@ -290,7 +296,7 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
     a.coords_out = coords1_out;
     a.flow_out = flow_out;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return hip_rc(chain ? (pair ? rc_launch_lookup_pair(a, radius, s)
+    return hip_rc(chain ? (pair ? rc_launch_lookup_pair(a, radius, pyr_dtype == RC_BF16, s)
                                 : rc_launch_lookup_chain(a, radius, s))
                         : rc_launch_lookup(a, radius, pyr_dtype == RC_BF16, s),
                   "rc_corr_lookup_step: launch");

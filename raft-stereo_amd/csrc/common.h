@@ -76,6 +76,8 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
     __bf16 b = (__bf16)f;
     return __builtin_bit_cast(uint16_t, b);
 }
+// fp32 value rounded to bf16 precision (RNE), kept in fp32.
+__device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
 
 // Kernel parameter blocks (passed by value).
 struct BuildArgs {
@@ -151,7 +153,7 @@ hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, h
 hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf16, const float *w,
                                  const float *b, int cout, int relu, float *out, hipStream_t s);
 hipError_t rc_launch_lookup_chain(const rc::LookupArgs &a, int radius, hipStream_t s);
-hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, hipStream_t s);
+hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s);
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s);
 hipError_t rc_launch_convex_upsample(const float *flow, const float *mask, int N, int C, int H,

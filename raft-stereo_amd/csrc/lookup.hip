@@ -436,15 +436,27 @@ __global__ __launch_bounds__(256) void lookup_chain_kernel(LookupArgs a) {
 // 16 16-B loads per lane, and with fewer selects.  Window elements outside
 // [0, W_level) are zeroed once per level, which is exactly the reference's
 // per-tap zero padding (a tap reads window elements x0 and x0+1 only).
-template <int R>
+template <int R, bool BF16 = false>
 struct PairSpan {
     static constexpr int NW = 2 * R + 4;              // window elements per level
     static constexpr int NS = 2 * NW;                 // span elements
-    static constexpr int NC = (NS + 2 + 3) / 4;       // 16-B chunks (start misaligned by 0 or 2)
-    f32x4 q[NC];
+    static constexpr int EPC = BF16 ? 8 : 4;          // elements per 16-B chunk
+    static constexpr int ES = BF16 ? 2 : 4;           // element bytes
+    // the span starts at an even element: misaligned by 0, 2, .., EPC-2
+    static constexpr int NC = (NS + EPC - 2 + EPC - 1) / EPC;
+    uint32_t q[NC][4];                                // raw chunks
     float m, n;                                       // window centres of the odd / even level
-    int sh;                                           // span start - chunk base: 0 or 2
+    int sh;                                           // span start - chunk base (elements)
     bool inwin, valid;
+    // element e of the loaded chunks, as fp32
+    __device__ __forceinline__ float elem(int e) const {
+        if constexpr (BF16) {
+            const uint32_t u = q[e >> 3][(e & 7) >> 1];
+            return __builtin_bit_cast(float, (e & 1) ? (u & 0xFFFF0000u) : (u << 16));
+        } else {
+            return __builtin_bit_cast(float, q[e >> 2][e & 3]);
+        }
+    }
 };
 
 // Exact element range [f, l] (clipped to [0, W-1]) the taps of one level read.
@@ -458,10 +470,10 @@ __device__ __forceinline__ void tap_span(float xl, int W, int &f, int &l) {
     l = min((int)floorf(pb) + 1, W - 1);
 }
 
-template <int R>
-__device__ __forceinline__ void issue_pair(PairSpan<R> &ps, const LookupArgs &a, int lo, float x,
+template <int R, bool BF16 = false>
+__device__ __forceinline__ void issue_pair(PairSpan<R, BF16> &ps, const LookupArgs &a, int lo, float x,
                                            long long pblk, long long lrow) {
-    typedef PairSpan<R> PS;
+    typedef PairSpan<R, BF16> PS;
     const int Wlo = a.W[lo], Whi = a.W[lo + 1];
     const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
     // false for NaN; outside it every tap of both levels is zero padding
@@ -479,18 +491,21 @@ __device__ __forceinline__ void issue_pair(PairSpan<R> &ps, const LookupArgs &a,
         if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
     }
     const int sa = 2 * ((int)ps.m - R - 1);
-    const int ea = sa & ~3;
+    const int ea = sa & ~(PS::EPC - 1);
     ps.sh = sa - ea;
     const long long ld = a.ld[lo];
-    const float *lvl = static_cast<const float *>(a.lvl[lo]);
-    const auto rs = make_rsrc(lvl + pblk * ld, clamp_bytes((a.P - pblk) * ld * 4));
+    const char *lvl = static_cast<const char *>(a.lvl[lo]);
+    const auto rs = make_rsrc(lvl + pblk * ld * PS::ES, clamp_bytes((a.P - pblk) * ld * PS::ES));
 #pragma unroll
     for (int k = 0; k < PS::NC; ++k) {
-        const int cs = ea + 4 * k;
+        const int cs = ea + PS::EPC * k;
         // lo_e >= 0 and hi_e < Wlo: a loaded chunk starts inside the row and
-        // ends inside its 16-B padded extent (ld % 4 == 0)
-        const bool ok = cs <= hi_e && cs + 3 >= lo_e;
-        ps.q[k] = ld4(rs, ok ? (uint32_t)((lrow * ld + cs) * 4) : 0xFFFFFF00u);
+        // ends inside its 16-B padded extent (ld % EPC == 0)
+        const bool ok = cs <= hi_e && cs + PS::EPC - 1 >= lo_e;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, ok ? (int)(uint32_t)((lrow * ld + cs) * PS::ES) : (int)0xFFFFFF00u, 0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ps.q[k][c] = v[c];
     }
 }
 
@@ -534,8 +549,20 @@ __device__ __forceinline__ void window_taps(const float *w, float xl, float nwin
 // The memory path for a lane whose level pair breaks the span relation
 // n = 2m + dd (only a subnormal x can): every tap re-read, level-i element k
 // = pool of S consecutive span-level elements.
-template <int R, int S>
-__device__ __forceinline__ void level_taps_mem(const float *row, float xl, int W, float *res) {
+// level-i element k (S consecutive bf16 span-level elements, each level of
+// the chain rounded to bf16 as stored)
+template <int S>
+__device__ __forceinline__ float derived_elem_bf16(const uint16_t *row, long long k) {
+    if constexpr (S == 1) {
+        return bf16_to_f32(row[k]);
+    } else {
+        const float a = derived_elem_bf16<S / 2>(row, 2 * k), b = derived_elem_bf16<S / 2>(row, 2 * k + 1);
+        return round_bf16((a + b) * 0.5f);
+    }
+}
+
+template <int R, int S, bool BF16 = false>
+__device__ __forceinline__ void level_taps_mem(const void *rowv, float xl, int W, float *res) {
     constexpr int T = 2 * R + 1;
     const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
     const DivRN dv = div_prep(Wm1);
@@ -547,32 +574,43 @@ __device__ __forceinline__ void level_taps_mem(const float *row, float xl, int W
         const float w1 = xp - x0, w0 = 1.0f - w1;
         const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
         const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
-        const float v0 = ok0 ? derived_elem<S>(row, (long long)x0) : 0.0f;
-        const float v1 = ok1 ? derived_elem<S>(row, (long long)x0 + 1) : 0.0f;
+        float v0 = 0.0f, v1 = 0.0f;
+        if constexpr (BF16) {
+            const uint16_t *row = static_cast<const uint16_t *>(rowv);
+            if (ok0) v0 = derived_elem_bf16<S>(row, (long long)x0);
+            if (ok1) v1 = derived_elem_bf16<S>(row, (long long)x0 + 1);
+        } else {
+            const float *row = static_cast<const float *>(rowv);
+            if (ok0) v0 = derived_elem<S>(row, (long long)x0);
+            if (ok1) v1 = derived_elem<S>(row, (long long)x0 + 1);
+        }
         res[t] = fmaf(w1, v1, w0 * v0);
     }
 }
 
-template <int R, bool NOFALLBACK = false, class Sink>
-__device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupArgs &a, int lo,
+template <int R, bool NOFALLBACK = false, bool BF16 = false, class Sink>
+__device__ __forceinline__ void finish_pair(const PairSpan<R, BF16> &ps, const LookupArgs &a, int lo,
                                             float x, long long pp, Sink &&sink) {
-    typedef PairSpan<R> PS;
-    constexpr int T = 2 * R + 1, NW = PS::NW, NS = PS::NS;
+    typedef PairSpan<R, BF16> PS;
+    constexpr int T = 2 * R + 1, NW = PS::NW, NS = PS::NS, EPC = PS::EPC;
     const int Wlo = a.W[lo], Whi = a.W[lo + 1];
-    // span element j = chunk element j + sh, sh in {0, 2}
+    // span element j = chunk element j + sh, sh in {0, 2, .., EPC-2}
     float s[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-        const float v0 = ps.q[j >> 2][j & 3];
-        const float v2 = ps.q[(j + 2) >> 2][(j + 2) & 3];
-        s[j] = ps.sh ? v2 : v0;
+        float v = ps.elem(j);
+#pragma unroll
+        for (int d = 2; d < EPC; d += 2)
+            if (j + d < PS::NC * EPC) v = (ps.sh == d) ? ps.elem(j + d) : v;
+        s[j] = v;
     }
     const int mi = (int)ps.m - R - 1, ni = (int)ps.n - R - 1;
     const int dd = (int)ps.n - 2 * (int)ps.m;
     float wodd[NW], weven[NW];
 #pragma unroll
     for (int jj = 0; jj < NW; ++jj) {
-        const float pm = (s[2 * jj] + s[2 * jj + 1]) * 0.5f;      // model.py:294 in fp32
+        float pm = (s[2 * jj] + s[2 * jj + 1]) * 0.5f;      // model.py:294 in fp32
+        if constexpr (BF16) pm = round_bf16(pm);           // the odd level as stored
         wodd[jj] = (unsigned)(mi + jj) < (unsigned)Whi ? pm : 0.0f;
         const float e = dd == 0 ? s[R + 1 + jj] : s[R + 2 + jj];
         weven[jj] = (unsigned)(ni + jj) < (unsigned)Wlo ? e : 0.0f;
@@ -582,9 +620,9 @@ __device__ __forceinline__ void finish_pair(const PairSpan<R> &ps, const LookupA
     window_taps<R>(weven, xlo, ps.n, Wlo, r0);
     window_taps<R>(wodd, xhi, ps.m, Whi, r1);
     if (!NOFALLBACK && __builtin_expect(ps.inwin && !ps.valid, 0)) {   // subnormal x only
-        const float *row = static_cast<const float *>(a.lvl[lo]) + pp * a.ld[lo];
-        level_taps_mem<R, 1>(row, xlo, Wlo, r0);
-        level_taps_mem<R, 2>(row, xhi, Whi, r1);
+        const char *row = static_cast<const char *>(a.lvl[lo]) + pp * a.ld[lo] * PS::ES;
+        level_taps_mem<R, 1, BF16>(row, xlo, Wlo, r0);
+        level_taps_mem<R, 2, BF16>(row, xhi, Whi, r1);
     }
 #pragma unroll
     for (int t = 0; t < T; ++t) sink(lo * T + t, r0[t]);
@@ -622,19 +660,19 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
 // flight (26.6 us, 198 VGPRs).
 // M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-202, dev library):
 // 1 = no output stores, 2 = no fallback path.
-template <int R, int NL, int M = 0>
+template <int R, int NL, int M = 0, bool BF16 = false>
 __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
     constexpr int NP = NL / 2;                        // spans per pixel
     const PairPixel q = pair_pixel<R, NL>(a, (long long)blockIdx.x * 256);
-    PairSpan<R> sp[NP];
+    PairSpan<R, BF16> sp[NP];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) issue_pair<R>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
+    for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
     auto sink = [&](int ch, float v) {
         if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
     };
 #pragma unroll
-    for (int k = 0; k < NP; ++k) finish_pair<R, M == 2>(sp[k], a, 2 * k, q.x, q.pp, sink);
+    for (int k = 0; k < NP; ++k) finish_pair<R, M == 2, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink);
 }
 
 #ifdef RAFTCORR_DEV
@@ -686,7 +724,7 @@ __global__ __launch_bounds__(256) void lookup_pair_stamped_kernel(LookupArgs a) 
 #endif
 
 template <int R>
-static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
+static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
 #ifdef RAFTCORR_DEV
     if constexpr (R == 4) {
@@ -702,12 +740,15 @@ static hipError_t launch_pair_r(const LookupArgs &a, hipStream_t s) {
         }
     }
 #endif
-    if (a.levels == 4)
-        hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
-    else if (a.levels == 2)
-        hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
-    else
+    if (a.levels == 4) {
+        if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+    } else if (a.levels == 2) {
+        if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+    } else {
         return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -881,13 +922,13 @@ hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, h
     }
 }
 
-hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, hipStream_t s) {
+hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;
     switch (radius) {
-        case 1: return rc::launch_pair_r<1>(a, s);
-        case 2: return rc::launch_pair_r<2>(a, s);
-        case 3: return rc::launch_pair_r<3>(a, s);
-        case 4: return rc::launch_pair_r<4>(a, s);
+        case 1: return rc::launch_pair_r<1>(a, pyr_bf16, s);
+        case 2: return rc::launch_pair_r<2>(a, pyr_bf16, s);
+        case 3: return rc::launch_pair_r<3>(a, pyr_bf16, s);
+        case 4: return rc::launch_pair_r<4>(a, pyr_bf16, s);
         default: return hipErrorInvalidValue;
     }
 }

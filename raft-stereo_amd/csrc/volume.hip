@@ -217,6 +217,11 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
             for (int nb = 0; nb < 4; ++nb) {
                 const float v = acc[ma][nb][r];
                 c[nb] = a.pow2 ? v * a.scale : v / a.sq;
+                // a bf16 pyramid pools each level from the level below AS
+                // STORED (bf16), like avg_pool2d on a bf16 tensor and like
+                // rc_corr_pool: the pool-chain lookups can then derive a
+                // level from a stored one bit for bit
+                if (bf) c[nb] = round_bf16(c[nb]);
             }
             if constexpr (MODE & kModeNoStores) {
                 float keep = c[0] + c[1] + c[2] + c[3];
@@ -235,15 +240,17 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
             }
             if (a.nfused < 2) continue;
             // level 1 (lane-local pairs), staged in this wave's LDS image [R][32]
-            *reinterpret_cast<f32x2 *>(stA + R * 32 + 2 * col) =
-                f32x2{(c[0] + c[1]) * 0.5f, (c[2] + c[3]) * 0.5f};
+            f32x2 l1 = {(c[0] + c[1]) * 0.5f, (c[2] + c[3]) * 0.5f};
+            if (bf) l1 = f32x2{round_bf16(l1[0]), round_bf16(l1[1])};
+            *reinterpret_cast<f32x2 *>(stA + R * 32 + 2 * col) = l1;
         }
     }
     if constexpr (!(MODE & kModeNoStores)) {
         if (a.nfused < 2) return;
         // Levels >= 1 from the wave-private LDS images (in-order LDS within a
         // wave: no barrier needed).  Level l+1 = pairwise mean of level l,
-        // read back from LDS in fp32: the same ops as avg_pool2d (:294).
+        // read back from LDS in fp32: the same ops as avg_pool2d (:294)
+        // (bf16 pyramid: of level l rounded to bf16, as stored).
         // a NULL level is computed (the next one needs it) but not stored
         if (a.lvl[1]) store_staged_any<FM>(stA, 1, a.lvl[1], a.ld[1], bf, rowbase, m0, n0, W1, W2 >> 1, lane);
         float *src = stA, *dst = stB;
@@ -253,7 +260,8 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
             for (int idx = lane; idx < FM * 16 * cw; idx += 64) {
                 const int R = idx >> lcw, j = idx & (cw - 1);
                 const f32x2 pr = *reinterpret_cast<const f32x2 *>(src + R * cwp + 2 * j);
-                dst[R * cw + j] = (pr[0] + pr[1]) * 0.5f;
+                const float pm = (pr[0] + pr[1]) * 0.5f;
+                dst[R * cw + j] = bf ? round_bf16(pm) : pm;
             }
             if (a.lvl[l]) store_staged_any<FM>(dst, l, a.lvl[l], a.ld[l], bf, rowbase, m0, n0, W1, W2 >> l, lane);
             float *t = src;

@@ -222,13 +222,65 @@ def test_chain_block_stores_two_levels():
         assert len(blk.corr_pyramid) == 5 and blk.levels_stored == [0, 1, 2, 3, 4]
 
 
-def test_chain_not_used_for_bf16_or_other_levels():
+def test_chain_not_used_for_other_levels():
     f = torch.randn(1, 8, 2, 64, device=DEV)
     with torch.no_grad():
-        assert not CorrBlock1D(f, f, num_levels=4, pyramid_dtype=torch.bfloat16)._chain
+        assert CorrBlock1D(f, f, num_levels=4, pyramid_dtype=torch.bfloat16)._chain
+        assert not CorrBlock1D(f, f, num_levels=3, pyramid_dtype=torch.bfloat16)._chain
         assert not CorrBlock1D(f, f, num_levels=1)._chain
         assert not CorrBlock1D(f, f, num_levels=5, radius=2)._chain
         assert not CorrBlock1D(f, f, num_levels=4, radius=5)._chain
+
+
+def bf16_pool_np(level):
+    """avg_pool2d([1,2]) of a bf16 level in fp32, rounded to bf16 (RNE), as
+    PyTorch computes it on bf16 tensors."""
+    t = torch.from_numpy(np.ascontiguousarray(level)).bfloat16().float()
+    Wo = t.shape[1] // 2
+    pm = (t[:, 0:2 * Wo:2] + t[:, 1:2 * Wo:2]) * 0.5
+    return pm.bfloat16().float().numpy()
+
+
+BF16_PAIR_SHAPES = [
+    # B, D, H, W1, W2, L, r
+    (2, 64, 3, 240, 240, 4, 4),
+    (1, 32, 2, 311, 311, 4, 4),     # config-3 width: odd level widths
+    (1, 16, 3, 45, 45, 4, 3),
+    (1, 16, 2, 50, 50, 2, 4),
+    (1, 8, 2, 20, 16, 4, 1),
+]
+
+
+@pytest.mark.parametrize("shape", BF16_PAIR_SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("fmap_dt", [torch.bfloat16, torch.float32], ids=["bf16in", "f32in"])
+def test_bf16_pair_lookup_bitexact(shape, fmap_dt):
+    """bf16 pyramid (config 3): every level is the bf16 pool of the level
+    below as stored (the build epilogue, rc_corr_pool and avg_pool2d on bf16
+    agree), and the pair kernel (levels 0 and 2 read, 1 and 3 derived and
+    rounded) equals the per-level lookup over the materialised bf16 pyramid
+    bit for bit, NaN/inf/subnormal coords included."""
+    B, D, H, W1, W2, L, r = shape
+    g = torch.Generator().manual_seed(700 + sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV, fmap_dt)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV, fmap_dt)
+    coords = special_coords(B, H, W1, W2, g).to(DEV)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=torch.bfloat16)
+        eager = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=torch.bfloat16,
+                            lazy_levels=False)
+        assert blk._chain and blk.levels_stored == ([0, 2] if L == 4 else [0])
+        a = blk(coords)
+        pyr = blk.corr_pyramid
+        b = rcorr.lookup(pyr, coords, L, r)
+        c = eager(coords)
+    assert same(a.cpu().numpy(), b.cpu().numpy())
+    assert same(a.cpu().numpy(), c.cpu().numpy())
+    lv = pyr_np(blk)
+    le = pyr_np(eager)
+    for i in range(L + 1):
+        assert same(lv[i], le[i]), f"lazy vs fused epilogue, level {i}"
+        if i:
+            assert same(lv[i], bf16_pool_np(lv[i - 1])), f"level {i} != bf16 pool of level {i - 1}"
 
 
 def test_repeat_launches_deterministic():
