@@ -82,3 +82,42 @@ extern "C" int rc_dev_gather_probe(const float *table, long long nrows, int row,
     }
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
+
+// Alignment probe (dev only): what a 16-B buffer load returns at byte offsets
+// 0, 2, 4, 6, 8 -- into VGPRs (mode 0), by LDS DMA (mode 1), and 4-B LDS DMA
+// (mode 2).  One wave; lane l loads at offset 64*l + shift; out[l][4] dwords
+// per shift.
+namespace {
+__global__ __launch_bounds__(64) void align_probe_kernel(const char *src, unsigned *out, int mode) {
+    __shared__ __attribute__((aligned(16))) unsigned lds[5][64 * 4];
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int lane = threadIdx.x;
+    const auto r = rc::make_rsrc(src, 64 * 64 + 64);
+    for (int s = 0; s < 5; ++s) {
+        const int off = 64 * lane + 2 * s;
+        if (mode == 0) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+            for (int k = 0; k < 4; ++k) lds[s][4 * lane + k] = v[k];
+        } else if (mode == 1) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)&lds[s][0], 16, off, 0, 0, 0);
+        } else {
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)&lds[s][64 * k], 4, off + 4 * k, 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < 5; ++s)
+        for (int k = 0; k < 4; ++k) {
+            // mode 2 wrote dword k of every lane contiguously per k
+            const unsigned v = mode == 2 ? lds[s][64 * k + lane] : lds[s][4 * lane + k];
+            out[(s * 64 + lane) * 4 + k] = v;
+        }
+}
+}  // namespace
+
+extern "C" int rc_dev_align_probe(const void *src, void *out, int mode, void *stream) {
+    hipLaunchKernelGGL(align_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       (const char *)src, (unsigned *)out, mode);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -33,7 +33,8 @@ namespace rc {
 
 // Dev-only ablation flags (RAFTCORR_BUILD_MODE): 1 = no operand loads,
 // 2 = no epilogue stores.  Product launches use 0.
-enum { kModeNoLoads = 1, kModeNoStores = 2, kModeStagger = 64 };
+enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8, kModeNoFragReads = 16,
+       kModeStagger = 64 };
 
 // First-round stagger: workgroup slot k of a CU (blockIdx / nCU) waits k
 // units before starting, so the co-resident workgroups of a CU sit in
@@ -529,6 +530,703 @@ __global__ __launch_bounds__(256) void build_bf16_kernel(BuildArgs a, int nwg_to
     wave_tile_bf16<IN_BF16, ALIGNED, MODE>(a, row, b, h, m0, n0, lane, img, stA, stB);
 }
 
+// ====== bf16 fmaps: persistent workgroups, shared LDS-DMA ring ======
+//
+// The per-wave staging above loads every operand tile twice per workgroup
+// (two waves share each A and each B tile) and re-reads each fmap row once
+// per 128-wide tile on the other side: at W = 311 that is ~7x the unique
+// fmap bytes through L1 per row, plus two loads and a shift per unaligned
+// chunk.  This kernel instead:
+//   * covers up to 320 w2 in one tile (2 x NWN waves, wave tile 64 w1 x
+//     16*FMA w2, FMA = 4 or 5 fragments), so per image row F2 is read
+//     ceil(W1/128) times and F1 once;
+//   * stages [32 d][cols] bf16 tiles of F1 and F2, shared by all waves, in an
+//     SL-slot ring filled by buffer->LDS DMA (no VGPR staging).  Each lane's
+//     16-B source is 8 consecutive w of one d-row at any 2-B alignment, so
+//     rows that do not start on a 16-B boundary (W = 311) need no shifting;
+//   * is persistent: one workgroup per CU walks its tiles and the ring runs on
+//     across tile boundaries, so the next tile's first stages are in flight
+//     while this tile's epilogue stores (the staging has its own LDS);
+//   * reads stage s+1's fragments while stage s's MFMAs run (two fragment
+//     register sets);
+//   * swaps the MFMA operands (A = F2: M = w2, B = F1: N = w1) so each lane's
+//     accumulator registers hold 4 CONSECUTIVE w2 of one w1: pyramid levels
+//     1-2 are lane-local poolings, 3-4 xor-16 / xor-32 lane exchanges -- all
+//     in registers, in the order avg_pool2d uses (model.py:294).  Each level
+//     is written in 16-row pieces through a wave-private fp32 image as
+//     whole-row vector stores.  (At most 5 fused levels; more are pooled by
+//     rc_launch_pool.)
+// LDS image rows are 256-B multiples, with 16-B chunk j of row r stored at
+// chunk j ^ 2*sigma(r), sigma(r) = (r & 3) | ((r >> 3) & 1) << 2: the eight
+// rows one half-wave's ds_read_b64_tr_b16 touches land on eight different
+// 32-B bank groups (conflict-free).  The DMA writes LDS lane-linearly, so
+// the swizzle is applied to each lane's SOURCE chunk; pad chunks get an
+// out-of-range (no-op) offset.
+//
+// vmcnt on gfx950 counts stores as well as loads, in issue order: a wait for
+// a ring stage must not also wait for the epilogue stores issued after that
+// stage's DMA.  Each wave counts the vector-memory instructions it issued
+// (vmq; stores counted at most once per store call, so never over-counted)
+// and waits for stage s with vmcnt(vmq - vmq at s's issue).
+constexpr int kB16BK = 32;                  // d rows per stage
+constexpr int kB16P1 = 256;                 // F1 image pitch: 128 w1
+constexpr int kB16MaxFused = 5;             // levels the ring epilogue writes
+constexpr int kB16DeferStage = 16 * 144;    // deferred epilogue: per-wave bf16 image of 16 rows
+
+template <int NWN, int FMA>
+struct B16Geom {
+    static constexpr int NW = 2 * NWN;                              // waves
+    static constexpr int WT = 16 * FMA;                             // wave tile w2 width
+    static constexpr int TW = WT * NWN;                             // workgroup tile w2 width
+    static constexpr int P2 = (2 * TW + 255) / 256 * 256;           // F2 image pitch (B)
+    static constexpr int C2 = P2 / 16, C1 = kB16P1 / 16;            // 16-B chunks per row
+    static constexpr int SLOT = kB16BK * (P2 + kB16P1);             // bytes per ring slot
+    static constexpr int NINS2 = kB16BK * C2 / 64;                  // F2 DMA instructions per stage
+    static constexpr int NINS = NINS2 + kB16BK * C1 / 64;           // all
+    static constexpr int IPW = (NINS + NW - 1) / NW;                // per wave (max)
+    static constexpr int STP = WT + 4;                              // level-0 staging pitch (floats)
+    static constexpr int STB = 16 * STP * 4;                        // staging bytes per wave
+    static_assert((kB16BK * C2) % 64 == 0 && (kB16BK * C1) % 64 == 0, "whole DMA pieces");
+    static_assert(C2 % 16 == 0, "swizzle groups");
+};
+
+__device__ __forceinline__ int b16_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+// ds_read_b64_tr_b16 as inline asm.  The compiler puts an s_waitcnt
+// vmcnt(0) (every LDS DMA in flight, the ring's prefetch included) in front
+// of any LDS access it sees while LDS DMA is pending; these reads are
+// ordered by the ring's own waits and barriers instead, and their results by
+// an lgkmcnt wait that names them.
+template <int OFF>
+__device__ __forceinline__ s16x4 tr_read_asm(uint32_t lds_addr) {
+    s16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(lds_addr), "i"(OFF));
+    return v;
+}
+
+// Pitch-parametrised fragment read (see read_frag): rows 8g+q and 8g+4+q.
+__device__ __forceinline__ bf16x8 read_frag_p(const char *p, int pitch) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p + 4 * pitch));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)(p);
+}
+
+// s_waitcnt vmcnt(m) lgkmcnt(0) with m = n rounded down to a multiple of 4,
+// capped at 60 (waiting for more than asked is always safe); the immediate
+// is chosen by a 4-deep branch tree on the wave-uniform n.
+template <int LO, int HI>
+__device__ __forceinline__ void wait_vm_tree(int m) {
+    if constexpr (LO == HI) {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(LO) : "memory");
+    } else {
+        constexpr int MID = (LO + HI) / 8 * 4;   // last multiple of 4 in the lower half
+        if (m <= MID) wait_vm_tree<LO, MID>(m);
+        else wait_vm_tree<MID + 4, HI>(m);
+    }
+}
+__device__ __forceinline__ void wait_vm_lgkm0(int n) {
+    const int m = n >= 60 ? 60 : (n < 0 ? 0 : n & ~3);
+    wait_vm_tree<0, 60>(m);
+}
+
+// The epilogue's wave-private staging accesses are inline asm too (see
+// tr_read_asm): in-order LDS execution within a wave orders them, and a
+// read's result is used only after the lgkmcnt(0) wait inside its asm.
+__device__ __forceinline__ void lds_st4(uint32_t a, f32x4 v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v));
+}
+__device__ __forceinline__ void lds_st2(uint32_t a, f32x2 v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v));
+}
+__device__ __forceinline__ void lds_st1(uint32_t a, float v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v));
+}
+
+// Rows [0, 16) of a wave's staged level image (fp32 at LDS address st,
+// pitch p floats, cw columns) -> level memory, VW elements per lane, cw / VW
+// lanes per row.  Adds to vmq the store calls some lane made (a lower bound
+// on the store instructions issued).
+template <int VW>
+__device__ __forceinline__ void store_rows16(uint32_t st, int p, int cw, void *lvl, long long ld,
+                                             bool bf16, long long rowbase, int w1_0, int col0, int W1,
+                                             int Wl, int lane, int &vmq) {
+    const int lpr = cw / VW;                 // lanes per row
+    const int rpi = 64 / lpr;                // rows per instruction
+    const int Rl = lane / lpr, j = (lane - Rl * lpr) * VW;
+    const int col = col0 + j;
+    for (int r0 = 0; r0 < 16; r0 += rpi) {
+        const int R = r0 + Rl, w1 = w1_0 + R;
+        const uint32_t src = st + 4 * (R * p + j);
+        float v[VW];
+        if constexpr (VW == 8) {
+            f32x4 x0, x1;
+            asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(x0), "=&v"(x1) : "v"(src));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) { v[c] = x0[c]; v[4 + c] = x1[c]; }
+        } else if constexpr (VW == 4) {
+            f32x4 x0;
+            asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x0) : "v"(src));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = x0[c];
+        } else if constexpr (VW == 2) {
+            f32x2 x0;
+            asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x0) : "v"(src));
+            v[0] = x0[0]; v[1] = x0[1];
+        } else {
+            float x0;
+            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x0) : "v"(src));
+            v[0] = x0;
+        }
+        const bool ok = Rl < rpi && R < 16 && w1 < W1 && col < Wl;
+        if (ok) store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v);
+        vmq += __builtin_amdgcn_ballot_w64(ok) != 0 ? 1 : 0;
+    }
+}
+
+__device__ __forceinline__ void store_rows16_any(uint32_t st, int p, int cw, void *lvl, long long ld,
+                                                 bool bf16, long long rowbase, int w1_0, int col0,
+                                                 int W1, int Wl, int lane, int &vmq) {
+    // widest vector dividing the image width (col0 is a multiple of it) and
+    // the row stride
+    if (bf16 && ld % 8 == 0 && cw % 8 == 0)
+        store_rows16<8>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+    else if (ld % 4 == 0 && cw % 4 == 0)
+        store_rows16<4>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+    else if (ld % 2 == 0 && cw % 2 == 0)
+        store_rows16<2>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+    else
+        store_rows16<1>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+}
+
+__device__ __forceinline__ float pool2(float x, float y, bool bf) {
+    const float m = (x + y) * 0.5f;
+    return bf ? round_bf16(m) : m;
+}
+
+// Epilogue of the swapped-operand tile: acc[ma][nb] register r of lane l =
+// C[w1 = m0 + 16nb + (l&15)][w2 = n0 + 16ma + 4(l>>4) + r].  One fragment
+// column nb (16 w1 rows) at a time, every level: level l's image has rows
+// w1 - m0 - 16nb, columns (w2 - n0) >> l, pitch (WT >> l) + 4 floats.
+template <int FMA, int MODE, int NLM>
+__device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const BuildArgs &a, int row,
+                                                 int m0, int n0, int lane0, uint32_t st0, int &vmq) {
+    constexpr int WT = 16 * FMA;
+    const bool bf = a.pyr_bf16 != 0;
+    const long long rowbase = (long long)row * a.W1;
+    const int nl = a.nfused < NLM ? a.nfused : NLM;
+    // one loop body for the four columns (code size, registers): column nb
+    // is always acc[.][0], the others move down one per pass
+#pragma unroll 1
+    for (int nb = 0; nb < 4; ++nb) {
+        // opaque per pass: otherwise the compiler hoists the per-lane staging
+        // and store addresses of every level and vector width out of the
+        // loops and keeps ~100 of them in VGPRs
+        int lane = lane0;
+        uint32_t st = st0;
+        asm volatile("" : "+v"(lane), "+v"(st));
+        const int g = lane >> 4, i = lane & 15;
+        auto flush = [&](int l) {
+            const int cw = WT >> l;
+            store_rows16_any(st, cw + 4, cw, a.lvl[l], a.ld[l], bf, rowbase, m0 + 16 * nb, n0 >> l, a.W1,
+                             a.W2 >> l, lane, vmq);
+        };
+        float v[FMA][4];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float x = acc[ma][0][r];
+                const float c = a.pow2 ? x * a.scale : x / a.sq;
+                v[ma][r] = bf ? round_bf16(c) : c;
+            }
+            acc[ma][0] = acc[ma][1];
+            acc[ma][1] = acc[ma][2];
+            acc[ma][2] = acc[ma][3];
+        }
+        if constexpr (MODE & kModeNoStores) {
+            float keep = 0.f;
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma) keep += v[ma][0] + v[ma][3];
+            asm volatile("" ::"v"(keep));
+            continue;
+        }
+        if (a.lvl[0]) {
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma)
+                lds_st4(st + 4 * (i * (WT + 4) + 16 * ma + 4 * g), f32x4{v[ma][0], v[ma][1], v[ma][2], v[ma][3]});
+            flush(0);
+        }
+        if (nl < 2) continue;
+        // level 1: lane-local pairs of w2
+        float u[FMA][2];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+            u[ma][0] = pool2(v[ma][0], v[ma][1], bf);
+            u[ma][1] = pool2(v[ma][2], v[ma][3], bf);
+        }
+        if (a.lvl[1]) {
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma)
+                lds_st2(st + 4 * (i * (WT / 2 + 4) + 8 * ma + 2 * g), f32x2{u[ma][0], u[ma][1]});
+            flush(1);
+        }
+        if (nl < 3) continue;
+        // level 2: lane-local
+        float s2[FMA];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) s2[ma] = pool2(u[ma][0], u[ma][1], bf);
+        if (a.lvl[2]) {
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma) lds_st1(st + 4 * (i * (WT / 4 + 4) + 4 * ma + g), s2[ma]);
+            flush(2);
+        }
+        if (nl < 4) continue;
+        // level 3: lanes l, l^16 (w2 groups g, g^1); the even-g lane stores it
+        float s3[FMA];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+            const float o = __shfl_xor(s2[ma], 16);
+            s3[ma] = (g & 1) ? pool2(o, s2[ma], bf) : pool2(s2[ma], o, bf);
+        }
+        if (a.lvl[3]) {
+            if (!(g & 1)) {
+#pragma unroll
+                for (int ma = 0; ma < FMA; ++ma) lds_st1(st + 4 * (i * (WT / 8 + 4) + 2 * ma + (g >> 1)), s3[ma]);
+            }
+            flush(3);
+        }
+        if (nl < 5) continue;
+        // level 4: lanes l, l^32 (g = 0 with g = 2)
+        float s4[FMA];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+            const float o = __shfl_xor(s3[ma], 32);
+            s4[ma] = (g & 2) ? pool2(o, s3[ma], bf) : pool2(s3[ma], o, bf);
+        }
+        if (a.lvl[4]) {
+            if (g == 0) {
+#pragma unroll
+                for (int ma = 0; ma < FMA; ++ma) lds_st1(st + 4 * (i * (WT / 16 + 4) + ma), s4[ma]);
+            }
+            flush(4);
+        }
+    }
+}
+
+// One tile of the persistent walk: its image row and workgroup origin.
+struct B16Tile {
+    int row, b, h, M0, N0;
+};
+
+// 2*NWN compute waves + 2 loader waves.  Only the loader waves issue the
+// ring's DMA, and only the compute waves store: vmcnt on gfx950 counts
+// loads and stores together, and a load may complete after a later store,
+// so a wave that had stored could wait for its DMA only by waiting for its
+// stores too.  Each stage: loaders wait for their DMA of stage gs ->
+// barrier -> loaders refill the slot stage gs-1 used; compute waves read
+// stage gs's fragments and run its MFMAs (and a tile's epilogue after its
+// last stage) -- their lgkmcnt(0) before the next barrier releases the slot.
+template <int NWN, int FMA, int SL, int MODE, int NLM, bool DEFER>
+__global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildArgs a, int ntiles, int tiles_m,
+                                                                           int tiles_n) {
+    typedef B16Geom<NWN, FMA> G;
+    constexpr int NC = G::NW;                                     // compute waves
+    constexpr int LIPW = G::NINS / 2;                             // DMA instructions per loader wave per stage
+    static_assert(G::NINS % 2 == 0 && LIPW * (SL - 1) + 2 <= 60, "loader vmcnt budget");
+    static_assert(!DEFER || FMA == 4, "deferred epilogue: 4 fragments per wave");
+    __shared__ __attribute__((aligned(16))) char smem[SL * G::SLOT + NC * (DEFER ? kB16DeferStage : G::STB)];
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int D = a.D, H = a.H, W1 = a.W1, W2 = a.W2;
+    const int T = tiles_m * tiles_n;
+
+    // Persistent walk, XCD-aware: workgroup v runs on XCD v % 8; the tiles
+    // are cut into 8 contiguous runs, one per XCD, in proportion to its
+    // workgroups, which take them round-robin -- so the tiles of one image
+    // row run at the same time on one XCD and share its L2 copy of the row.
+    const int nwg = gridDim.x, v = blockIdx.x;
+    const int xcd = v & 7, lw = v >> 3;
+    const int gx = (nwg - xcd + 7) >> 3;                          // workgroups on this XCD
+    const int before = xcd * (nwg >> 3) + min(xcd, nwg & 7);      // workgroups on lower XCDs
+    const int t0 = (int)((long long)ntiles * before / nwg);
+    const int t1 = (int)((long long)ntiles * (before + gx) / nwg);
+    auto tile_at = [&](int k) {                                   // k-th tile of this workgroup
+        B16Tile t;
+        const int id = t0 + lw + k * gx;
+        t.row = id / T;
+        const int tl = id - t.row * T, tm = tl / tiles_n, tn = tl - tm * tiles_n;
+        t.b = t.row / H;
+        t.h = t.row - t.b * H;
+        t.M0 = tm * 128;
+        t.N0 = tn * G::TW;
+        return t;
+    };
+    const int ntile_mine = t0 + lw < t1 ? (t1 - t0 - lw + gx - 1) / gx : 0;
+    if (ntile_mine == 0) return;                                  // workgroup-uniform
+    const long long img1 = (long long)D * H * W1, img2 = (long long)D * H * W2;
+    const int nst = (D + kB16BK - 1) / kB16BK;                    // >= 2 (launcher)
+    const int total = ntile_mine * nst;
+
+    if (wave >= NC) {
+        // ------------------------------ loader ------------------------------
+        const int lid = wave - NC;                                // its instructions: ins = lid + 2k
+        const uint32_t sstep2 = (uint32_t)((long long)kB16BK * H * W2 * 2);
+        const uint32_t sstep1 = (uint32_t)((long long)kB16BK * H * W1 * 2);
+        // per lane and instruction: d row, logical (unswizzled) source chunk,
+        // tile-independent source offset
+        int dr[LIPW], dj[LIPW];
+        uint32_t dbase[LIPW];
+#pragma unroll
+        for (int k = 0; k < LIPW; ++k) {
+            const int ins = lid + 2 * k;
+            const bool f2 = ins < G::NINS2;
+            const int c = f2 ? 64 * ins + lane : 64 * (ins - G::NINS2) + lane;
+            const int rd = f2 ? c / G::C2 : c / G::C1;
+            const int j = (c - rd * (f2 ? G::C2 : G::C1)) ^ b16_swz(rd);
+            dr[k] = rd;
+            dj[k] = f2 && 8 * j >= G::TW ? 1 << 20 : j;           // F2 pad chunks never load
+            dbase[k] = (uint32_t)((rd * H * (f2 ? W2 : W1) + 8 * j) * 2);
+        }
+        __amdgpu_buffer_rsrc_t ir1 = make_rsrc(a.f1, 0), ir2 = make_rsrc(a.f2, 0);
+        // stage-0 source offsets; kOOB (past any image: num_records < 2^31,
+        // and adding the stage steps keeps it there) = nothing to load
+        constexpr uint32_t kOOB = 0x80000000u;
+        uint32_t tb[LIPW];
+        B16Tile it;
+        auto set_issue_tile = [&](const B16Tile &t) {
+            it = t;
+            ir1 = make_rsrc(reinterpret_cast<const char *>(a.f1) + t.b * img1 * 2, clamp_bytes(img1 * 2));
+            ir2 = make_rsrc(reinterpret_cast<const char *>(a.f2) + t.b * img2 * 2, clamp_bytes(img2 * 2));
+            const uint32_t o2 = (uint32_t)((t.h * W2 + t.N0) * 2), o1 = (uint32_t)((t.h * W1 + t.M0) * 2);
+#pragma unroll
+            for (int k = 0; k < LIPW; ++k) {
+                constexpr int K2 = G::NINS2 / 2;                    // k < K2: an F2 instruction (NINS2 even)
+                const bool ok = k < K2 ? t.N0 + 8 * dj[k] < W2 : t.M0 + 8 * dj[k] < W1;
+                tb[k] = ok ? dbase[k] + (k < K2 ? o2 : o1) : kOOB;
+            }
+        };
+        // A 16-B DMA source that is only 2-B aligned is range-checked per 4-B
+        // piece counted from its start, so the piece holding the LAST element
+        // of an image (d = D-1, h = H-1, w = W-1) and the element after it
+        // reads as zero.  The lane that DMAs that chunk loads the element (in
+        // range) just before the stage's DMA and writes it into LDS once the
+        // stage has landed: (LDS offset << 16 | value), ~0 = none.
+        uint32_t pp[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+        int pp_gs = -1;
+        int vmq = 0, q[SL], nq = 0;                                // loads issued; vmq after each pending stage
+        auto issue = [&](int gs, int st) {
+            char *slot = smem + (gs % SL) * G::SLOT;
+            if (st == nst - 1 && it.h == H - 1) {
+                const int rd = (D - 1) % kB16BK;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const bool f2 = t == 0;
+                    const int Wt = f2 ? W2 : W1, org = f2 ? it.N0 : it.M0, span = f2 ? G::TW : 128;
+                    if (Wt - 1 < org || Wt - 1 >= org + span) continue;
+                    const int j = (Wt - 1 - org) >> 3, p = j ^ b16_swz(rd);
+                    const int c = f2 ? rd * G::C2 + p : G::NINS2 * 64 + rd * G::C1 + p;
+                    if ((c >> 6) % 2 != lid) continue;              // wave-uniform
+                    if ((c & 63) == lane) {
+                        const unsigned short val = __builtin_amdgcn_raw_buffer_load_b16(
+                            f2 ? ir2 : ir1, (int)((((long long)(D - 1) * H + it.h) * Wt + Wt - 1) * 2), 0, 0);
+                        pp[t] = ((uint32_t)(16 * c + 2 * ((Wt - 1 - org) & 7)) << 16) | val;
+                    }
+                    ++vmq;
+                    pp_gs = gs;
+                }
+            }
+            const int dlim = D - kB16BK * st;                      // rows d >= D read zeros
+            const uint32_t s2 = (uint32_t)st * sstep2, s1 = (uint32_t)st * sstep1;
+#pragma unroll
+            for (int k = 0; k < LIPW; ++k) {
+                constexpr int K2 = G::NINS2 / 2;
+                uint32_t o = tb[k] + (k < K2 ? s2 : s1);
+                if (dlim < kB16BK && dr[k] >= dlim) o = kOOB;      // only a last stage with D % 32 != 0
+                if constexpr ((MODE & kModeAlignedSrc) != 0) o &= ~15u;   // dev timing only: wrong data
+                if constexpr ((MODE & kModeNoLoads) == 0)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(k < K2 ? ir2 : ir1,
+                                                             (lds_void *)(slot + 1024 * (lid + 2 * k)), 16, (int)o,
+                                                             0, 0, 0);
+            }
+            if constexpr ((MODE & kModeNoLoads) == 0) vmq += LIPW;
+#pragma unroll
+            for (int x = 0; x < SL; ++x)
+                if (x == nq) q[x] = vmq;
+            ++nq;
+        };
+        int issued = 0, it_k = 0, it_st = 0;
+        auto issue_next = [&]() {
+            if (issued >= total) return;
+            issue(issued, it_st);
+            ++issued;
+            if (++it_st == nst) {
+                it_st = 0;
+                if (++it_k < ntile_mine) set_issue_tile(tile_at(it_k));
+            }
+        };
+        set_issue_tile(tile_at(0));
+#pragma unroll
+        for (int s = 0; s < SL - 1; ++s) issue_next();
+        for (int gs = 0; gs < total; ++gs) {
+            // stage gs landed: every load issued up to its DMA is done
+            // (loads complete in order)
+            wait_vm_lgkm0(vmq - q[0]);
+#pragma unroll
+            for (int x = 0; x + 1 < SL; ++x) q[x] = q[x + 1];
+            --nq;
+            if (gs == pp_gs) {
+                char *slotp = smem + (gs % SL) * G::SLOT;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    if (pp[t] != 0xFFFFFFFFu)
+                        *reinterpret_cast<unsigned short *>(slotp + (pp[t] >> 16)) = (unsigned short)pp[t];
+                    pp[t] = 0xFFFFFFFFu;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            issue_next();
+        }
+        return;
+    }
+
+    // ------------------------------ compute ------------------------------
+    // transposed-read addresses of this lane inside a slot (row 8g+q, 4 cols
+    // of fragment f, swizzled); the k = 8g+4.. rows are +4 rows (same swizzle)
+    const int gq = (lane >> 4) & 3, qq = (lane >> 2) & 3, p4 = lane & 3;
+    const int rr = 8 * gq + qq, sw = b16_swz(rr);
+    const int wm = wave & 1, wn = wave >> 1;
+    const uint32_t a_row = rr * G::P2 + 8 * (p4 & 1), b_row = kB16BK * G::P2 + rr * kB16P1 + 8 * (p4 & 1);
+    const int a_ch = (G::WT / 8) * wn + (p4 >> 1), b_ch = 8 * wm + (p4 >> 1);
+    const uint32_t stg = lds_u32(smem + SL * G::SLOT + wave * G::STB);
+    int vmq_unused = 0;
+    f32x4 acc[FMA][4];
+    // DEFER (bf16 pair layout: levels 0 and 2): a finished tile's levels are
+    // held in registers as packed bf16 and stored one piece (16 rows) every
+    // nst/4 stages during the next tile's K loop, so the stores overlap the
+    // ring's loads instead of stalling the workgroup between tiles.  Level 2
+    // is stored when the tile ends, after a lane transpose that gives lane
+    // (g, i) the 4 level-2 values of fragment ma = g.
+    uint32_t h0[FMA][4][2];
+    int hrow = 0, hm0 = 0, hn0 = 0;
+    bool hact = false, held = false;
+    const int g = lane >> 4, i16 = lane & 15;
+    auto hold = [&](int row, int m0h, int n0h, bool act) {
+        hrow = row; hm0 = m0h; hn0 = n0h; hact = act; held = true;
+        if (!act) return;
+        float s2[FMA][4];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                float vv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float x = acc[ma][nb][r];
+                    vv[r] = round_bf16(a.pow2 ? x * a.scale : x / a.sq);
+                }
+                h0[ma][nb][0] = pack_bf16x2(vv[0], vv[1]);
+                h0[ma][nb][1] = pack_bf16x2(vv[2], vv[3]);
+                if constexpr ((MODE & kModeNoStores) != 0)       // dev timing: keep the MFMAs alive
+                    asm volatile("" ::"v"(h0[ma][nb][0]), "v"(h0[ma][nb][1]));
+                s2[ma][nb] = pool2(pool2(vv[0], vv[1], true), pool2(vv[2], vv[3], true), true);
+            }
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+            float qv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                // source side: this lane offers its s2 of fragment (g - r) & 3;
+                // it receives from lane group (g + r) & 3 that group's value
+                // of fragment g
+                const int ms = (g - r) & 3;
+                const float x = ms == 0 ? s2[0][nb] : ms == 1 ? s2[1][nb] : ms == 2 ? s2[2][nb] : s2[3][nb];
+                const int src = (g + r) & 3;
+                const float y = r ? __shfl(x, i16 + 16 * src) : x;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) qv[j] = src == j ? y : qv[j];
+            }
+            // level 2 is small (8 B per lane and column): stored right away
+            const int w1 = m0h + 16 * nb + i16, col = (n0h >> 2) + 4 * g;
+            if (!(MODE & kModeNoStores) && w1 < W1 && col < (W2 >> 2))
+                *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(a.lvl[2]) +
+                                           ((long long)row * W1 + w1) * a.ld[2] + col) =
+                    uint2{pack_bf16x2(qv[0], qv[1]), pack_bf16x2(qv[2], qv[3])};
+        }
+    };
+    // piece nb = level-0 rows 16nb..16nb+15 of the held tile: staged as bf16
+    // in this wave's LDS image (16 rows x 128 B, pitch 144 B) and stored as
+    // whole 128-B row segments, 16 B per lane -- 8-B stores straight from
+    // the registers would write each line in four pieces at different times
+    // (measured 1.5x the HBM write bytes)
+    auto store_piece = [&](int nb) {
+        if (!hact) return;
+        // opaque per piece, so that the addresses of all pieces are not
+        // precomputed per tile and kept live through the K loop
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int g = ln >> 4, i16 = ln & 15;
+        char *img = smem + SL * G::SLOT + wave * kB16DeferStage;
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma)
+            *reinterpret_cast<uint2 *>(img + i16 * 144 + (16 * ma + 4 * g) * 2) = uint2{h0[ma][nb][0], h0[ma][nb][1]};
+        uint16_t *l0 = reinterpret_cast<uint16_t *>(a.lvl[0]);
+        const long long rowbase = (long long)hrow * W1;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int R = 8 * half + (ln >> 3), c = ln & 7;
+            const uint4 x = *reinterpret_cast<const uint4 *>(img + R * 144 + 16 * c);
+            const int w1 = hm0 + 16 * nb + R, col = hn0 + 8 * c;
+            if (w1 < W1 && col < W2) *reinterpret_cast<uint4 *>(l0 + (rowbase + w1) * a.ld[0] + col) = x;
+        }
+    };
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int x = 0; x < FMA; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    int k = 0, st = 0;
+    B16Tile cur = tile_at(0);
+    int m0 = cur.M0 + 64 * wm, n0 = cur.N0 + G::WT * wn;         // this wave's w1 / w2 origin
+    bool active = m0 < W1 && n0 < W2;                             // wave-uniform
+    zero_acc();
+    for (int gs = 0; gs < total; ++gs) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (active && !(MODE & kModeNoMath)) {
+            // compiler-visible LDS reads are fine here: no LDS DMA is ever
+            // pending on the compute waves' path, so no vmcnt wait is added,
+            // and the compiler pairs each fragment's two reads in one tuple
+            const char *slot = smem + (gs % SL) * G::SLOT;
+            bf16x8 fa[FMA], fb[4];
+            if constexpr ((MODE & kModeNoFragReads) != 0) {    // dev timing only: MFMAs on stale registers
+#pragma unroll
+                for (int f = 0; f < FMA; ++f) { fa[f] = bf16x8{}; asm volatile("" : "+v"(fa[f])); }
+#pragma unroll
+                for (int f = 0; f < 4; ++f) { fb[f] = bf16x8{}; asm volatile("" : "+v"(fb[f])); }
+            } else {
+#pragma unroll
+                for (int f = 0; f < FMA; ++f) fa[f] = read_frag_p(slot + a_row + 16 * ((a_ch + 2 * f) ^ sw), G::P2);
+#pragma unroll
+                for (int f = 0; f < 4; ++f) fb[f] = read_frag_p(slot + b_row + 16 * ((b_ch + 2 * f) ^ sw), kB16P1);
+            }
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma)
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ma], fb[nb], acc[ma][nb], 0, 0, 0);
+        }
+        if constexpr (DEFER && !(MODE & kModeNoStores)) {
+            if (held) {
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    if (((nb * nst) >> 2) == st) store_piece(nb);
+            }
+        }
+        if (++st == nst) {
+            if constexpr (DEFER) hold(cur.row, m0, n0, active);
+            else if (active) epilogue_swapped<FMA, MODE, NLM>(acc, a, cur.row, m0, n0, lane, stg, vmq_unused);
+            st = 0;
+            if (++k < ntile_mine) {
+                cur = tile_at(k);
+                m0 = cur.M0 + 64 * wm;
+                n0 = cur.N0 + G::WT * wn;
+                active = m0 < W1 && n0 < W2;
+                zero_acc();
+            }
+        }
+    }
+    if constexpr (DEFER && !(MODE & kModeNoStores)) {
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) store_piece(nb);
+    }
+}
+
+// (waves along w2, fragments per wave, deferred epilogue) for the ring
+// kernel: the fewest padded w2 columns per row, ties to the wider tile;
+// nwn = 0: use the per-wave kernel.  The deferred (register-held) epilogue
+// serves the bf16 pair layout (levels 0 and 2 stored, level 1 not) with
+// 8-B-aligned rows; it uses 64-wide wave tiles, up to 5 along w2.
+struct B16Shape { int nwn, fma; bool defer; };
+static B16Shape bf16_ring_shape(const BuildArgs &a) {
+    if (a.W2 <= 64 || (a.D + kB16BK - 1) / kB16BK < 2) return {0, 0, false};
+    // 32-bit source offsets with an out-of-range marker at 2^31
+    if ((long long)a.D * a.H * (a.W1 > a.W2 ? a.W1 : a.W2) * 2 >= (1LL << 30)) return {0, 0, false};
+    if (a.nfused > kB16MaxFused)              // levels past the ring's are pooled from memory
+        for (int l = kB16MaxFused - 1; l < a.nfused; ++l)
+            if (!a.lvl[l]) return {0, 0, false};
+    const bool defer = a.pyr_bf16 && a.nfused == 3 && a.lvl[0] && !a.lvl[1] && a.lvl[2] && a.ld[0] % 8 == 0 &&
+                       a.ld[2] % 4 == 0;
+    static const B16Shape cand[] = {{4, 5, false}, {4, 4, false}, {3, 5, false}, {3, 4, false}, {2, 5, false},
+                                    {2, 4, false}};
+    static const B16Shape cand_defer[] = {{5, 4, true}, {4, 4, true}, {3, 4, true}, {2, 4, true}};
+    B16Shape best = {0, 0, false};
+    long long bestpad = 0;
+    auto consider = [&](const B16Shape &c) {
+        const long long w = 16LL * c.fma * c.nwn, pad = (a.W2 + w - 1) / w * w;
+        if (!best.nwn || pad < bestpad) { best = c; bestpad = pad; }
+    };
+    if (defer)
+        for (const B16Shape &c : cand_defer) consider(c);
+    else
+        for (const B16Shape &c : cand) consider(c);
+    return best;
+}
+
+static int device_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+template <int NWN, int FMA, int SL, int MODE, bool DEFER>
+static void launch_bf16_ring_n(const BuildArgs &a, hipStream_t s) {
+    constexpr int TW = B16Geom<NWN, FMA>::TW;
+    const int tiles_m = (a.W1 + 127) / 128, tiles_n = (a.W2 + TW - 1) / TW;
+    const long long ntiles = (long long)a.B * a.H * tiles_m * tiles_n;
+    if (ntiles <= 0 || ntiles > 0x7FFFFFFF) return;
+    const long long nwg = ntiles < device_cus() ? ntiles : device_cus();   // one per CU (LDS-bound)
+    // up to 3 fused levels (the default pair layout) keeps the epilogue's
+    // level pointers out of the scalar registers the K loop needs
+    if (DEFER || a.nfused <= 3)
+        hipLaunchKernelGGL((build_bf16_ring_kernel<NWN, FMA, SL, MODE, 3, DEFER>), dim3((unsigned)nwg),
+                           dim3(128 * NWN + 128), 0, s, a, (int)ntiles, tiles_m, tiles_n);
+    else
+        hipLaunchKernelGGL((build_bf16_ring_kernel<NWN, FMA, SL, MODE, kB16MaxFused, DEFER>), dim3((unsigned)nwg),
+                           dim3(128 * NWN + 128), 0, s, a, (int)ntiles, tiles_m, tiles_n);
+}
+
+// the deferred-epilogue kernel has no staging area: 4 ring slots
+template <int MODE>
+static void launch_bf16_ring(const BuildArgs &a, B16Shape sh, hipStream_t s) {
+    if (sh.defer) {
+        if (sh.nwn == 5) launch_bf16_ring_n<5, 4, 4, MODE, true>(a, s);
+        else if (sh.nwn == 4) launch_bf16_ring_n<4, 4, 4, MODE, true>(a, s);
+        else if (sh.nwn == 3) launch_bf16_ring_n<3, 4, 4, MODE, true>(a, s);
+        else launch_bf16_ring_n<2, 4, 4, MODE, true>(a, s);
+    } else if (sh.nwn == 4 && sh.fma == 5) launch_bf16_ring_n<4, 5, 3, MODE, false>(a, s);
+    else if (sh.nwn == 4) launch_bf16_ring_n<4, 4, 3, MODE, false>(a, s);
+    else if (sh.nwn == 3 && sh.fma == 5) launch_bf16_ring_n<3, 5, 3, MODE, false>(a, s);
+    else if (sh.nwn == 3) launch_bf16_ring_n<3, 4, 3, MODE, false>(a, s);
+    else if (sh.fma == 5) launch_bf16_ring_n<2, 5, 3, MODE, false>(a, s);
+    else launch_bf16_ring_n<2, 4, 3, MODE, false>(a, s);
+}
+
 // ============ fp32 MFMA with a workgroup LDS-DMA ring (default) ============
 //
 // Operand tiles are shared by the workgroup's four waves through a 3-slot LDS
@@ -709,11 +1407,41 @@ static void launch_bf16(const BuildArgs &a, unsigned nwg, hipStream_t s) {
 
 }  // namespace rc
 
-hipError_t rc_launch_build_bf16mma(const rc::BuildArgs &a, int in_bf16, hipStream_t s) {
+// bf16 MFMA build.  The ring kernel fuses at most kB16MaxFused levels:
+// a.nfused is lowered to what was written, and the caller pools the rest.
+hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s) {
     const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     const unsigned n = (unsigned)nwg;
+    rc::B16Shape sh = in_bf16 ? rc::bf16_ring_shape(a) : rc::B16Shape{0, 0, false};
+#ifdef RAFTCORR_DEV
+    // 32: per-wave kernel; ring ablations (timing only, all without epilogue
+    // stores): 40 product, 41 no DMA, 44 no fragment reads / MFMA, 45
+    // neither, 48 16-B-aligned (wrong) DMA sources
+    const int mode = rc::dev_knob("RAFTCORR_BUILD_MODE");
+    if (mode == 32) sh = rc::B16Shape{0, 0, false};
+    if (sh.nwn && mode >= 40 && mode <= 48) {
+        if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
+        switch (mode) {
+            case 40: rc::launch_bf16_ring<2>(a, sh, s); break;
+            case 41: rc::launch_bf16_ring<3>(a, sh, s); break;
+            case 44: rc::launch_bf16_ring<6>(a, sh, s); break;
+            case 45: rc::launch_bf16_ring<7>(a, sh, s); break;
+            case 42: rc::launch_bf16_ring<18>(a, sh, s); break;   // no stores, MFMA without fragment reads
+            case 43: rc::launch_bf16_ring<19>(a, sh, s); break;   // ... and no DMA
+            case 46: rc::launch_bf16_ring<1>(a, sh, s); break;   // no DMA, with stores
+            case 47: rc::launch_bf16_ring<5>(a, sh, s); break;   // no DMA, no MFMA, with stores
+            default: rc::launch_bf16_ring<10>(a, sh, s); break;
+        }
+        return hipGetLastError();
+    }
+#endif
+    if (sh.nwn) {
+        if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
+        rc::launch_bf16_ring<0>(a, sh, s);
+        return hipGetLastError();
+    }
     if (in_bf16) {
         if (a.W1 % 8 == 0 && a.W2 % 8 == 0) rc::launch_bf16<true, true>(a, n, s);
         else rc::launch_bf16<true, false>(a, n, s);

@@ -300,6 +300,10 @@ BF16_SHAPES = [
     (2, 256, 2, 311, 311, 4, 4),    # config-3 width: rows not 16-B aligned
     (1, 96, 3, 40, 57, 3, 3),       # D % 32 != 0, odd W2
     (1, 37, 2, 24, 33, 4, 2),
+    # bf16-fmap ring kernel: 4 waves along w2 x 3 w2 tiles, 6 w1 tiles
+    (1, 64, 2, 700, 720, 4, 4),
+    (1, 256, 1, 150, 130, 3, 4),    # 3 waves along w2; idle waves in the last w1 tile
+    (1, 40, 2, 100, 100, 4, 2),     # 2 waves along w2, D % 32 != 0
 ]
 
 
@@ -533,3 +537,41 @@ def test_lookup_step_matches_unfused(L, r, pyr_dt):
         corr2, new2, _ = blk.lookup_step(buf, delta, out=buf)
         assert new2.data_ptr() == buf.data_ptr() and torch.equal(buf, ref_new)
         assert same(corr2.cpu().numpy(), corr.cpu().numpy())
+
+
+RING_SHAPES = [
+    # B, D, H, W1, W2, L  (L + 1 = 7 buffers: every level in the fused epilogue)
+    (1, 64, 2, 130, 200, 6),
+    (2, 32, 2, 67, 311, 6),
+    (1, 48, 3, 311, 311, 6),
+]
+
+
+@pytest.mark.parametrize("shape", RING_SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("pyr_dt", [torch.float32, torch.bfloat16], ids=["f32pyr", "bf16pyr"])
+def test_bf16_ring_epilogue_all_levels(shape, pyr_dt, monkeypatch):
+    """bf16 fmaps take the LDS-DMA ring kernel, whose epilogue pools levels
+    1-6 in registers (lane-local, xor-16, xor-32, fragment pairs).  Eager
+    build of 7 levels: level 0 vs the oracle, every level i >= 1 == the pool
+    of level i-1 as stored (corr_pool / bf16 avg_pool2d) bit for bit, and the
+    per-wave bf16 kernel (dev library, RAFTCORR_BUILD_MODE=32) gives the same
+    bits."""
+    B, D, H, W1, W2, L = shape
+    g = torch.Generator().manual_seed(99 + sum(shape))
+    f1 = torch.randn(B, D, H, W1, generator=g).bfloat16()
+    f2 = torch.randn(B, D, H, W2, generator=g).bfloat16()
+    with torch.no_grad():
+        blk = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=2, pyramid_dtype=pyr_dt,
+                          lazy_levels=False)
+        got = pyr_np(blk)
+        monkeypatch.setenv("RAFTCORR_BUILD_MODE", "32")
+        with _lib.dev_library():
+            old = pyr_np(CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=2,
+                                     pyramid_dtype=pyr_dt, lazy_levels=False))
+    ref = coracle.corr_pyramid(f1.float().numpy(), f2.float().numpy(), 0)[0]
+    assert norm_err(got[0], ref) <= (1e-5 if pyr_dt == torch.float32 else 8e-3)
+    for i in range(1, L + 1):
+        want = coracle.corr_pool(got[i - 1]) if pyr_dt == torch.float32 else bf16_pool_np(got[i - 1])
+        assert same(got[i], want), f"level {i}"
+    for i in range(L + 1):
+        assert same(got[i], old[i]), f"ring vs per-wave kernel, level {i}"

@@ -1,6 +1,6 @@
 """Mean per dispatch of every rocprofv3 counter, per kernel.
 
-    python tools/pmc_raw.py <pmc_dir>
+    python tools/pmc_raw.py <pmc_dir> [--width N]   (kernel-name characters kept, default 48)
 """
 import csv
 import glob
@@ -9,14 +9,14 @@ import sys
 from collections import defaultdict
 
 
-def main(d):
+def main(d, width=48):
     agg = defaultdict(lambda: defaultdict(float))
     names, times = {}, {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
             k = int(r["Dispatch_Id"])
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            names[k] = r["Kernel_Name"].split("(")[0][:48]
+            names[k] = r["Kernel_Name"].split("(")[0][:width]
             times[k] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     per = defaultdict(list)
     for k in sorted(agg):
@@ -29,4 +29,5 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    w = int(sys.argv[sys.argv.index("--width") + 1]) if "--width" in sys.argv else 48
+    main(sys.argv[1], w)
