@@ -536,38 +536,33 @@ __global__ __launch_bounds__(256) void build_bf16_kernel(BuildArgs a, int nwg_to
 // (two waves share each A and each B tile) and re-reads each fmap row once
 // per 128-wide tile on the other side: at W = 311 that is ~7x the unique
 // fmap bytes through L1 per row, plus two loads and a shift per unaligned
-// chunk.  This kernel instead:
-//   * covers up to 320 w2 in one tile (2 x NWN waves, wave tile 64 w1 x
-//     16*FMA w2, FMA = 4 or 5 fragments), so per image row F2 is read
+// chunk (1.80 ms at config 3, B = 64).  This kernel instead:
+//   * covers up to 320 w2 in one tile (2 x NWN compute waves, wave tile 64
+//     w1 x 16*FMA w2, FMA = 4 or 5 fragments), so per image row F2 is read
 //     ceil(W1/128) times and F1 once;
 //   * stages [32 d][cols] bf16 tiles of F1 and F2, shared by all waves, in an
-//     SL-slot ring filled by buffer->LDS DMA (no VGPR staging).  Each lane's
-//     16-B source is 8 consecutive w of one d-row at any 2-B alignment, so
-//     rows that do not start on a 16-B boundary (W = 311) need no shifting;
+//     SL-slot ring filled by buffer->LDS DMA from two loader waves (no VGPR
+//     staging).  Each lane's 16-B source is 8 consecutive w of one d-row at
+//     any 2-B alignment, so rows that do not start on a 16-B boundary
+//     (W = 311) need no shifting;
 //   * is persistent: one workgroup per CU walks its tiles and the ring runs on
-//     across tile boundaries, so the next tile's first stages are in flight
-//     while this tile's epilogue stores (the staging has its own LDS);
-//   * reads stage s+1's fragments while stage s's MFMAs run (two fragment
-//     register sets);
+//     across tile boundaries;
 //   * swaps the MFMA operands (A = F2: M = w2, B = F1: N = w1) so each lane's
 //     accumulator registers hold 4 CONSECUTIVE w2 of one w1: pyramid levels
 //     1-2 are lane-local poolings, 3-4 xor-16 / xor-32 lane exchanges -- all
-//     in registers, in the order avg_pool2d uses (model.py:294).  Each level
-//     is written in 16-row pieces through a wave-private fp32 image as
-//     whole-row vector stores.  (At most 5 fused levels; more are pooled by
-//     rc_launch_pool.)
+//     in registers, in the order avg_pool2d uses (model.py:294);
+//   * for the bf16 pair layout (levels 0 and 2 stored) defers the epilogue:
+//     a finished tile's level 0 is held in registers as packed bf16 and
+//     stored 16 rows at a time during the next tile's K loop, overlapping
+//     the ring's loads; other layouts write every level (at most 5 fused;
+//     more are pooled by rc_launch_pool) in 16-row pieces through a
+//     wave-private fp32 image right after the tile.
 // LDS image rows are 256-B multiples, with 16-B chunk j of row r stored at
 // chunk j ^ 2*sigma(r), sigma(r) = (r & 3) | ((r >> 3) & 1) << 2: the eight
 // rows one half-wave's ds_read_b64_tr_b16 touches land on eight different
 // 32-B bank groups (conflict-free).  The DMA writes LDS lane-linearly, so
 // the swizzle is applied to each lane's SOURCE chunk; pad chunks get an
 // out-of-range (no-op) offset.
-//
-// vmcnt on gfx950 counts stores as well as loads, in issue order: a wait for
-// a ring stage must not also wait for the epilogue stores issued after that
-// stage's DMA.  Each wave counts the vector-memory instructions it issued
-// (vmq; stores counted at most once per store call, so never over-counted)
-// and waits for stage s with vmcnt(vmq - vmq at s's issue).
 constexpr int kB16BK = 32;                  // d rows per stage
 constexpr int kB16P1 = 256;                 // F1 image pitch: 128 w1
 constexpr int kB16MaxFused = 5;             // levels the ring epilogue writes
@@ -650,12 +645,11 @@ __device__ __forceinline__ void lds_st1(uint32_t a, float v) {
 
 // Rows [0, 16) of a wave's staged level image (fp32 at LDS address st,
 // pitch p floats, cw columns) -> level memory, VW elements per lane, cw / VW
-// lanes per row.  Adds to vmq the store calls some lane made (a lower bound
-// on the store instructions issued).
+// lanes per row.
 template <int VW>
 __device__ __forceinline__ void store_rows16(uint32_t st, int p, int cw, void *lvl, long long ld,
                                              bool bf16, long long rowbase, int w1_0, int col0, int W1,
-                                             int Wl, int lane, int &vmq) {
+                                             int Wl, int lane) {
     const int lpr = cw / VW;                 // lanes per row
     const int rpi = 64 / lpr;                // rows per instruction
     const int Rl = lane / lpr, j = (lane - Rl * lpr) * VW;
@@ -686,23 +680,22 @@ __device__ __forceinline__ void store_rows16(uint32_t st, int p, int cw, void *l
         }
         const bool ok = Rl < rpi && R < 16 && w1 < W1 && col < Wl;
         if (ok) store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v);
-        vmq += __builtin_amdgcn_ballot_w64(ok) != 0 ? 1 : 0;
     }
 }
 
 __device__ __forceinline__ void store_rows16_any(uint32_t st, int p, int cw, void *lvl, long long ld,
                                                  bool bf16, long long rowbase, int w1_0, int col0,
-                                                 int W1, int Wl, int lane, int &vmq) {
+                                                 int W1, int Wl, int lane) {
     // widest vector dividing the image width (col0 is a multiple of it) and
     // the row stride
     if (bf16 && ld % 8 == 0 && cw % 8 == 0)
-        store_rows16<8>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+        store_rows16<8>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
     else if (ld % 4 == 0 && cw % 4 == 0)
-        store_rows16<4>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+        store_rows16<4>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
     else if (ld % 2 == 0 && cw % 2 == 0)
-        store_rows16<2>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+        store_rows16<2>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
     else
-        store_rows16<1>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, vmq);
+        store_rows16<1>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
 }
 
 __device__ __forceinline__ float pool2(float x, float y, bool bf) {
@@ -716,7 +709,7 @@ __device__ __forceinline__ float pool2(float x, float y, bool bf) {
 // w1 - m0 - 16nb, columns (w2 - n0) >> l, pitch (WT >> l) + 4 floats.
 template <int FMA, int MODE, int NLM>
 __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const BuildArgs &a, int row,
-                                                 int m0, int n0, int lane0, uint32_t st0, int &vmq) {
+                                                 int m0, int n0, int lane0, uint32_t st0) {
     constexpr int WT = 16 * FMA;
     const bool bf = a.pyr_bf16 != 0;
     const long long rowbase = (long long)row * a.W1;
@@ -735,7 +728,7 @@ __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const Bui
         auto flush = [&](int l) {
             const int cw = WT >> l;
             store_rows16_any(st, cw + 4, cw, a.lvl[l], a.ld[l], bf, rowbase, m0 + 16 * nb, n0 >> l, a.W1,
-                             a.W2 >> l, lane, vmq);
+                             a.W2 >> l, lane);
         };
         float v[FMA][4];
 #pragma unroll
@@ -1007,7 +1000,6 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
     const uint32_t a_row = rr * G::P2 + 8 * (p4 & 1), b_row = kB16BK * G::P2 + rr * kB16P1 + 8 * (p4 & 1);
     const int a_ch = (G::WT / 8) * wn + (p4 >> 1), b_ch = 8 * wm + (p4 >> 1);
     const uint32_t stg = lds_u32(smem + SL * G::SLOT + wave * G::STB);
-    int vmq_unused = 0;
     f32x4 acc[FMA][4];
     // DEFER (bf16 pair layout: levels 0 and 2): a finished tile's levels are
     // held in registers as packed bf16 and stored one piece (16 rows) every
@@ -1135,7 +1127,7 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
         }
         if (++st == nst) {
             if constexpr (DEFER) hold(cur.row, m0, n0, active);
-            else if (active) epilogue_swapped<FMA, MODE, NLM>(acc, a, cur.row, m0, n0, lane, stg, vmq_unused);
+            else if (active) epilogue_swapped<FMA, MODE, NLM>(acc, a, cur.row, m0, n0, lane, stg);
             st = 0;
             if (++k < ntile_mine) {
                 cur = tile_at(k);

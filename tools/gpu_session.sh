@@ -39,6 +39,13 @@ has ablatek && step ablate_kitti 600 python tools/ablate.py --config kitti --bui
 has configs && step bench_realtime 300 python bench.py --config realtime --no-cpu-baseline --steps 50 --warmup 5 && step bench_realtime_graph 300 python bench.py --config realtime --graph --no-cpu-baseline --steps 200 --warmup 10
 has configs && step bench_middlebury 300 python bench.py --config middlebury --no-cpu-baseline --steps 5 --warmup 2
 has configs && step bench_kitti 300 python bench.py --config kitti --no-cpu-baseline --steps 10 --warmup 3
+has kitti && step bench_kitti 300 python bench.py --config kitti --no-cpu-baseline --steps 10 --warmup 3
+if has profk; then
+    step rocprof_kitti 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o trace \
+        -- python3 bench.py --config kitti --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0
+    find "$OUT/profk" -name "*stats*.csv" -exec sh -c 'echo "== $1"; cat "$1"' _ {} \; > "$OUT/kernel_stats_kitti.txt" 2>/dev/null
+    head -c 2000 "$OUT/kernel_stats_kitti.txt"
+fi
 if has prof; then
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace \
         -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0
