@@ -467,9 +467,10 @@ __global__ __launch_bounds__(256) void lookup_bwd_pair_kernel(LookupBwdArgs a) {
 
 // ---------------------------------------------------------------- volume bwd
 
-// Reduction elements per stage KS = 32 (LDS rows of 40 floats) or 16 (rows
-// of 24): both strides keep every 16-lane group of a ds_read_b128 on
-// distinct banks.  The stage holds KS/8 quads per thread and operand.
+// Reduction elements per stage KS = 16 (LDS rows of 24 floats; the product
+// choice) or 32 (rows of 40; dev A/B): both strides keep every 16-lane
+// group of a ds_read_b128 on distinct banks.  The stage holds KS/8 quads
+// per thread and operand.
 template <int KS>
 struct BwdTile {
     static constexpr int ROW = KS == 32 ? 40 : 24;   // floats per LDS image row
@@ -766,18 +767,33 @@ hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s) {
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     const bool vec = (a.W1 % 4 == 0) && (a.W2 % 4 == 0);
     const dim3 grid((unsigned)nwg), blk(256);
-    // two buffers stage K = 32 per barrier; more levels need more fold
-    // registers per staged quad, so they stage 16
+    // 16-k stages for every level count: 49 KB of LDS lets three workgroups
+    // share a CU (round 1 staged 32 for 1-2 levels: 851 / 976 us vs 718 /
+    // 862 us at config 2 with 1 / 2 levels, the same bits)
 #define RC_VBWD(NL)                                                                                 \
-    if (vec) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, NL, (NL == 1 || NL == 2) ? 32 : 16>),  \
-                                grid, blk, 0, s, a, (int)nwg);                                      \
-    else hipLaunchKernelGGL((rc::volume_bwd_kernel<false, NL, (NL == 1 || NL == 2) ? 32 : 16>),     \
-                            grid, blk, 0, s, a, (int)nwg);
-    if (a.nlev == 3 && a.g[1] == nullptr) {   // pair-folded gradients (levels 0 and 2)
-        if (vec) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, rc::kPairFold, 32>), grid, blk, 0, s, a, (int)nwg);
-        else hipLaunchKernelGGL((rc::volume_bwd_kernel<false, rc::kPairFold, 32>), grid, blk, 0, s, a, (int)nwg);
+    if (vec) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, NL, 16>), grid, blk, 0, s, a, (int)nwg); \
+    else hipLaunchKernelGGL((rc::volume_bwd_kernel<false, NL, 16>), grid, blk, 0, s, a, (int)nwg);
+    // pair-folded gradients (levels 0 and 2): 16-k stages, 49 KB of LDS, so
+    // three workgroups share a CU (784 vs 906 us for 32-k stages at config 2,
+    // the same bits)
+    if (a.nlev == 3 && a.g[1] == nullptr) {
+#ifdef RAFTCORR_DEV
+        if (vec && rc::dev_knob("RAFTCORR_VBWD_VARIANT") == 32) {   // dev A/B: 32-k stages (82 KB LDS)
+            hipLaunchKernelGGL((rc::volume_bwd_kernel<true, rc::kPairFold, 32>), grid, blk, 0, s, a, (int)nwg);
+            return hipGetLastError();
+        }
+#endif
+        if (vec) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, rc::kPairFold, 16>), grid, blk, 0, s, a, (int)nwg);
+        else hipLaunchKernelGGL((rc::volume_bwd_kernel<false, rc::kPairFold, 16>), grid, blk, 0, s, a, (int)nwg);
         return hipGetLastError();
     }
+#ifdef RAFTCORR_DEV
+    if (vec && rc::dev_knob("RAFTCORR_VBWD_VARIANT") == 32 && (a.nlev == 1 || a.nlev == 2)) {   // dev A/B
+        if (a.nlev == 1) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, 1, 32>), grid, blk, 0, s, a, (int)nwg);
+        else hipLaunchKernelGGL((rc::volume_bwd_kernel<true, 2, 32>), grid, blk, 0, s, a, (int)nwg);
+        return hipGetLastError();
+    }
+#endif
     switch (a.nlev) {   // the level count fixes the fold's loads at compile time
         case 1: RC_VBWD(1) break;
         case 2: RC_VBWD(2) break;

@@ -49,6 +49,8 @@ def main():
                     help="time the backward kernels")
     ap.add_argument("--bwd-variants", default="0,1,7",
                     help="RAFTCORR_LOOKUP_BWD_VARIANT values (0 product, 1 per-level waits, 3 capped occupancy, 4/5 prefetch 1/2 levels ahead, 6 grad_out loaded per level, 7 non-temporal grad_out loads)")
+    ap.add_argument("--vbwd-variants", default="0",
+                    help="RAFTCORR_VBWD_VARIANT values for the pair-layout volume backward (--bwd)")
     ap.add_argument("--convc1", action="store_true",
                     help="also time lookup+convc1+relu fused vs separate (MIOpen 1x1 conv)")
     a = ap.parse_args()
@@ -114,6 +116,7 @@ def main():
             go = torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev)
             gper = rcorr.grad_buffers(P, widths, dev)
             bv = [int(x) for x in a.bwd_variants.split(",") if x]
+            vv = [int(x) for x in a.vbwd_variants.split(",") if x]
             # bit-identity of the variants: same accumulation from the same start
             outs = {}
             for v in bv:
@@ -136,8 +139,29 @@ def main():
                 t = time_launches(lambda: rcorr.build_backward(f1, f2, gper), 2)
                 res.setdefault("volume_bwd", []).extend(t)
                 for nl in (1, 2):   # fewer levels to fold on load (what a pre-folded G would cost)
-                    t = time_launches(lambda: rcorr.build_backward(f1, f2, gper[:nl]), 2)
-                    res.setdefault(f"volume_bwd_nlev{nl}", []).extend(t)
+                    for v in vv:
+                        os.environ["RAFTCORR_VBWD_VARIANT"] = str(v)
+                        t = time_launches(lambda: rcorr.build_backward(f1, f2, gper[:nl]), 2)
+                        res.setdefault(f"volume_bwd_nlev{nl}_v{v}", []).extend(t)
+                    os.environ["RAFTCORR_VBWD_VARIANT"] = "0"
+            # the pair layout (the training default): RAFTCORR_VBWD_VARIANT values
+            gpair = rcorr.grad_buffers(P, widths, dev, pair=True)
+            for k in range(3):
+                rcorr.lookup_backward(gpair, coords[k], go, L, r)
+            ref_v = None
+            for v in vv:
+                os.environ["RAFTCORR_VBWD_VARIANT"] = str(v)
+                o = rcorr.build_backward(f1, f2, gpair)
+                if ref_v is None:
+                    ref_v = o
+                else:
+                    assert all(torch.equal(x, y) for x, y in zip(o, ref_v)), ("vbwd variant", v)
+            for rnd in range(a.rounds):
+                for v in vv:
+                    os.environ["RAFTCORR_VBWD_VARIANT"] = str(v)
+                    t = time_launches(lambda: rcorr.build_backward(f1, f2, gpair), 2)
+                    res.setdefault(f"volume_bwd_pair_v{v}", []).extend(t)
+            os.environ["RAFTCORR_VBWD_VARIANT"] = "0"
         if a.convc1:
             conv = torch.nn.Conv2d(L * (2 * r + 1), 64, 1).to(dev)
             base = ref_blk.lookup_convc1(coords[0], conv.weight, conv.bias)
