@@ -281,11 +281,13 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
 
     train_step()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    steps = []
+    for _ in range(max(reps, 9)):     # median of synchronised single steps (host jitter)
+        t0 = time.perf_counter()
         train_step()
-    torch.cuda.synchronize()
-    step_ms = (time.perf_counter() - t0) / reps * 1e3
+        torch.cuda.synchronize()
+        steps.append((time.perf_counter() - t0) * 1e3)
+    step_ms = sorted(steps)[len(steps) // 2]
     vflops = 2 * volume_flops(B, D, H, W1, W2)        # two GEMMs
     # x, grad_out, per-level window RMW (the layout-independent definition of
     # round 1; the pair layout's RMW touches 2 spans of 2(2r+4) elements instead)
@@ -514,7 +516,8 @@ def main():
         roof_volume = {"bound": "hbm", "achieved": vgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": vgbs / HBM_PEAK_GBS, "traffic": traffic.get("build_bytes"),
                        "algorithmic_bytes": vbytes, "flops": vflops,
-                       "kernel": "rc::build_bf16_kernel", "avg_launch_us": build_ms * 1e3,
+                       "kernel": ("rc::build_bf16_ring_kernel" if W2 > 64 else "rc::build_bf16_kernel"),
+                       "avg_launch_us": build_ms * 1e3,
                        "levels_written": written}
     else:
         roof_volume = {"bound": "mfma", "achieved": vflops / (build_ms * 1e-3) / 1e12,

@@ -46,6 +46,14 @@ if has profk; then
     find "$OUT/profk" -name "*stats*.csv" -exec sh -c 'echo "== $1"; cat "$1"' _ {} \; > "$OUT/kernel_stats_kitti.txt" 2>/dev/null
     head -c 2000 "$OUT/kernel_stats_kitti.txt"
 fi
+if has pmck; then   # kitti build HBM bytes (profiles/traffic.json "kitti")
+    step pmck_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmck_fetch" -o f \
+        -- python3 tools/build_probe.py --modes 0
+    step pmck_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmck_write" -o w \
+        -- python3 tools/build_probe.py --modes 0
+    python tools/pmc_traffic.py "$OUT/pmck_fetch" "$OUT/pmck_write" --config kitti --out "$OUT/traffic.json" > "$OUT/traffic_kitti.log" 2>&1
+    cat "$OUT/traffic_kitti.log"
+fi
 if has prof; then
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace \
         -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0
