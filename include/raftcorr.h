@@ -38,11 +38,30 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 4
+#define RC_ABI_VERSION 5
 
 /* element types */
 #define RC_F32  0
 #define RC_BF16 1
+
+/* Flags OR-ed into a pyr_dtype argument (ABI v5): RC_SHADOW_LEVEL(l) says
+ * stored pyramid level l has a line-phase SHADOW copy (RC_SHADOW: every
+ * stored level) -- the same rows, at byte offset
+ * RC_SHADOW_OFFSET(rows, ld, esize) from the level's base (rows = B*H*W1,
+ * ld = its row stride in elements, esize = 4 for RC_F32, 2 for RC_BF16), so
+ * the allocation holds rows*ld*esize bytes, a gap, then the copy, shifted by
+ * half a 128-byte line against the primary when the base is 128-B aligned.
+ * rc_corr_build writes both copies; the pair kernel of rc_corr_lookup_chain /
+ * rc_corr_lookup_step reads each pixel's span from the copy in which it
+ * touches fewer 128-B lines (bit-identical results, fewer HBM lines per
+ * pixel).  The other entry points accept the flag and read the primary copy.
+ * A level and its copy must fit in 4 GiB (RC_EUNSUPPORTED otherwise).  The
+ * copies cost build-time writes; which levels pay for themselves depends on
+ * the level's size and how often it is read. */
+#define RC_SHADOW_LEVEL(l) (0x100 << (l))
+#define RC_SHADOW 0xFF00
+#define RC_SHADOW_OFFSET(rows, ld, esize) \
+    ((((long long)(rows) * (long long)(ld) * (long long)(esize) + 127) / 128) * 128 + 64)
 
 /* return codes */
 #define RC_OK            0

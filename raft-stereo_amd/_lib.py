@@ -17,7 +17,18 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 RC_F32, RC_BF16 = 0, 1
 RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
-ABI_VERSION = 4
+ABI_VERSION = 5
+RC_SHADOW = 0xFF00  # pyr_dtype flags: every stored level carries a line-phase shadow copy
+
+
+def shadow_level(l):
+    """RC_SHADOW_LEVEL(l): pyr_dtype flag for a shadow copy of level l only."""
+    return 0x100 << l
+
+
+def shadow_offset(rows, ld, esize):
+    """RC_SHADOW_OFFSET: bytes from a stored level's base to its shadow copy."""
+    return -(-(rows * ld * esize) // 128) * 128 + 64
 
 # name -> (restype, argtypes); must match include/raftcorr.h exactly.
 _vp, _i, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_long

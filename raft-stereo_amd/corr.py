@@ -95,16 +95,45 @@ def _prep_fmap(f):
     return f.contiguous()
 
 
-def _level_buffer(P, W, dtype, device, pad):
+def _level_buffer(P, W, dtype, device, pad, shadow=False):
     """(P, 1, 1, W) tensor whose rows start 16-byte aligned: a view of a
     (P, ld) buffer with ld = W rounded up to 16 bytes when ``pad`` (the
-    kernels then store whole aligned vectors; the padding is never read)."""
-    per16 = 16 // torch.tensor([], dtype=dtype).element_size()
+    kernels then store whole aligned vectors; the padding is never read).
+    ``shadow``: the allocation also holds the level's RC_SHADOW copy at
+    ``_lib.shadow_offset`` bytes (include/raftcorr.h); the view is the primary."""
+    es = torch.tensor([], dtype=dtype).element_size()
+    per16 = 16 // es
     ld = -(-W // per16) * per16 if pad else W
-    buf = torch.empty((P, ld), dtype=dtype, device=device)
+    if shadow:
+        total = _lib.shadow_offset(P, ld, es) + P * ld * es
+        buf = torch.empty(-(-total // es), dtype=dtype, device=device)[:P * ld].view(P, ld)
+    else:
+        buf = torch.empty((P, ld), dtype=dtype, device=device)
     if ld == W:
         return buf.view(P, 1, 1, W)
     return buf[:, :W].unsqueeze(1).unsqueeze(1)
+
+
+def _shadow_levels(shadow, n):
+    """bool (every level) or an iterable of level indices -> frozenset."""
+    if shadow is True:
+        return frozenset(range(n))
+    if not shadow:
+        return frozenset()
+    return frozenset(int(l) for l in shadow if 0 <= int(l) < n)
+
+
+def _shadow_flags(levels, pyr):
+    """RC_SHADOW_LEVEL bits for the stored levels of ``pyr`` in ``levels``."""
+    return sum(_lib.shadow_level(l) for l in levels if l < len(pyr) and pyr[l] is not None)
+
+
+def shadow_fits(P, W, dtype):
+    """True when a level of width W and its RC_SHADOW copy fit the 4 GiB the
+    pair kernel addresses with 32-bit buffer offsets."""
+    es = torch.tensor([], dtype=dtype).element_size()
+    ld = -(-W // (16 // es)) * (16 // es)
+    return _lib.shadow_offset(P, ld, es) + P * ld * es <= 0xFFFFFF00
 
 
 def _row_stride(t):
@@ -114,11 +143,12 @@ def _row_stride(t):
     return t.stride(0) if t.shape[0] > 1 else t.shape[-1]
 
 
-def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, skip=()):
+def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, skip=(), shadow=False):
     """Run rc_corr_build: returns ``nbuf`` tensors (B*H*W1, 1, 1, W2 >> l)
     (row-padded views when ``pad``; values identical either way).  Levels in
     ``skip`` (>= 1) are computed by the fused epilogue but not stored: their
-    entries are None."""
+    entries are None.  ``shadow``: every stored level also gets its RC_SHADOW
+    copy (same values, half a 128-B line later; read by the pair lookup)."""
     B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
     if (W2 >> (nbuf - 1)) < 1:
         raise RuntimeError(
@@ -130,7 +160,8 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, ski
     if f1.dtype != f2.dtype:
         f1, f2 = f1.float(), f2.float()
     P = B * H * W1
-    pyr = [None if l in skip else _level_buffer(P, W2 >> l, pyramid_dtype, f1.device, pad)
+    shadow = _shadow_levels(shadow, nbuf) if pad else frozenset()
+    pyr = [None if l in skip else _level_buffer(P, W2 >> l, pyramid_dtype, f1.device, pad, l in shadow)
            for l in range(nbuf)]
     if P == 0:
         return pyr
@@ -139,7 +170,7 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, ski
             f1.data_ptr(), f2.data_ptr(), _dtype_code(f1.dtype), B, D, H, W1, W2,
             _lib.ptr_array([None if t is None else t.data_ptr() for t in pyr]),
             _lib.long_array([W2 >> l if t is None else _row_stride(t) for l, t in enumerate(pyr)]),
-            nbuf, _dtype_code(pyramid_dtype), _stream(f1.device))
+            nbuf, _dtype_code(pyramid_dtype) | _shadow_flags(shadow, pyr), _stream(f1.device))
     _lib.check(rc, "rc_corr_build")
     return pyr
 
@@ -240,12 +271,16 @@ def lookup(pyramid, coords, num_levels, radius):
     return out
 
 
-def _chain_args(pyramid, num_levels):
+def _chain_args(pyramid, num_levels, shadow=False):
     """Pointer / width / stride arrays for the pool-chain kernels: the levels
-    present in ``pyramid`` (None = recomputed by the kernel, passed as NULL)."""
+    present in ``pyramid`` (None = recomputed by the kernel, passed as NULL).
+    ``shadow``: levels built with their RC_SHADOW copy (build_pyramid's
+    ``shadow``); their flags are passed unless a level had to be copied."""
+    src = list(pyramid[:num_levels]) + [None] * (num_levels - len(pyramid))
     lv = [None if t is None else
           (t if t.stride(-1) == 1 and t.data_ptr() % 16 == 0 else t.contiguous())
-          for t in list(pyramid[:num_levels]) + [None] * (num_levels - len(pyramid))]
+          for t in src]
+    shadow = _shadow_levels(shadow, num_levels) if all(a is b for a, b in zip(lv, src)) else ()
     dt = lv[0].dtype
     if any(t is not None and t.dtype != dt for t in lv):
         raise TypeError("lookup_chain: pyramid levels of one dtype required")
@@ -253,10 +288,10 @@ def _chain_args(pyramid, num_levels):
     ptrs = _lib.ptr_array([None if t is None else t.data_ptr() for t in lv])
     widths = _lib.int_array([W0 >> i for i in range(num_levels)])
     lds = _lib.long_array([W0 >> i if t is None else _row_stride(t) for i, t in enumerate(lv)])
-    return lv, ptrs, widths, lds, _dtype_code(dt)
+    return lv, ptrs, widths, lds, _dtype_code(dt) | _shadow_flags(shadow, lv)
 
 
-def lookup_chain(pyramid, coords, num_levels, radius):
+def lookup_chain(pyramid, coords, num_levels, radius, shadow=False):
     """rc_corr_lookup_chain: same result as :func:`lookup` for a pyramid whose
     levels are the avg-pool chain of level 0 (what :func:`build_pyramid`
     writes).  Entries may be None: with 2 levels, or 4 levels and level 2
@@ -268,7 +303,7 @@ def lookup_chain(pyramid, coords, num_levels, radius):
                       device=coords.device)
     if B * H * W1 == 0:
         return out
-    keep, ptrs, widths, lds, dt = _chain_args(pyramid, num_levels)
+    keep, ptrs, widths, lds, dt = _chain_args(pyramid, num_levels, shadow)
     with torch.cuda.device(coords.device):
         rc = _lib.lib().rc_corr_lookup_chain(
             ptrs, widths, lds, dt, num_levels, radius, x.data_ptr(), cbs, B, H, W1,
@@ -345,6 +380,21 @@ def build_backward(fmap1, fmap2, grads):
     return df1, df2
 
 
+def default_shadow_levels(P, W2, num_levels, pyramid_dtype):
+    """Stored levels that get an RC_SHADOW copy by default (measured,
+    DESIGN.md §3.2e): level 2 of a 4-level pair layout always; level 0 only
+    when it is larger than the 256 MiB Infinity Cache -- a smaller level 0
+    mostly hits there across the loop's lookups, and a second copy would
+    double its cached footprint for a line saving it hardly needs (config 2:
+    l2 alone 1129 us per corr step, l0+l2 1140; config 3: l0+l2 6864, l2
+    alone 7013).  Each copy must fit the kernel's 4 GiB window."""
+    es = torch.tensor([], dtype=pyramid_dtype).element_size()
+    lv = [2] if num_levels == 4 else []
+    if P * W2 * es > (256 << 20):
+        lv.insert(0, 0)
+    return tuple(l for l in lv if shadow_fits(P, W2 >> l, pyramid_dtype))
+
+
 class _GradState:
     """Level gradients shared by one CorrBlock1D's lookup nodes and its build
     node.  Holds no pyramid and no graph node, so no reference cycle keeps the
@@ -405,7 +455,7 @@ class CorrBlock1D:
     """model.py:283-326, on the gfx950 kernels (see module docstring)."""
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
-                 lazy_levels=None):
+                 lazy_levels=None, shadow=None):
         self.num_levels = num_levels
         self.radius = radius
         if pyramid_dtype is None:
@@ -437,7 +487,16 @@ class CorrBlock1D:
                 nbuf, skip = (1, ()) if num_levels == 2 else (3, (1,))
             else:
                 nbuf, skip = num_levels + 1, ()
-            self._levels = build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype, skip=skip)
+            # RC_SHADOW: stored levels of the pair layout may
+            # get a half-line-shifted copy; the pair lookup reads each span
+            # from the copy where it touches fewer 128-B lines (same values).
+            # ``shadow``: None = the default levels, True/False, or indices.
+            pair = self._chain and num_levels in (2, 4) and lazy
+            if shadow is None:
+                shadow = default_shadow_levels(B * H * W1, W2, num_levels, pyramid_dtype)
+            self._shadow = _shadow_levels(shadow, nbuf) if pair else frozenset()
+            self._levels = build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype, skip=skip,
+                                         shadow=self._shadow)
             self._levels += [None] * (num_levels + 1 - nbuf)
         self._state = self._token = None
         if grad:
@@ -466,10 +525,11 @@ class CorrBlock1D:
         # a replaced pyramid need not be a pool chain: use the per-level lookup
         self._levels = list(levels)
         self._chain = False
+        self._shadow = frozenset()
 
     def _lookup(self, coords):
         if self._chain:
-            return lookup_chain(self._levels, coords, self.num_levels, self.radius)
+            return lookup_chain(self._levels, coords, self.num_levels, self.radius, self._shadow)
         return lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
 
     def __call__(self, coords):
@@ -513,7 +573,7 @@ class CorrBlock1D:
         if B * H * W1 == 0:
             return corr, new, flow
         if self._chain:
-            keep, ptrs, widths, lds, dt = _chain_args(self._levels, L)
+            keep, ptrs, widths, lds, dt = _chain_args(self._levels, L, self._shadow)
         else:
             keep, ptrs, widths, lds, dt = _level_args(self.corr_pyramid, L)
         with torch.cuda.device(c1.device):

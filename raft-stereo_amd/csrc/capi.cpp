@@ -31,6 +31,9 @@ int hip_rc(hipError_t e, const char *what) {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// RC_SHADOW (ABI v5): byte offset from a stored level's base to its copy.
+long long shadow_offset(long long rows, long long ld, int esize) { return RC_SHADOW_OFFSET(rows, ld, esize); }
+
 bool is_pow2_float(float v) {
     int e;
     return std::frexp(v, &e) == 0.5f;
@@ -54,8 +57,11 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
                              int H, int W1, int W2, void *const *pyr, const long *pyr_ld, int nbuf,
                              int pyr_dtype, void *stream) {
     g_err[0] = 0;
+    const unsigned shmask = ((unsigned)pyr_dtype >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits
+    pyr_dtype &= 0xFF;
     if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
         return fail(RC_EINVAL, "rc_corr_build: bad shape B=%d D=%d H=%d W1=%d W2=%d", B, D, H, W1, W2);
+
     if (nbuf < 1 || nbuf > RC_MAX_LEVELS)
         return fail(RC_EINVAL, "rc_corr_build: nbuf=%d outside 1..%d", nbuf, RC_MAX_LEVELS);
     if ((W2 >> (nbuf - 1)) < 1)
@@ -92,6 +98,8 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     for (int l = 0; l < a.nfused; ++l) {
         a.lvl[l] = pyr[l];
         a.ld[l] = pyr_ld ? pyr_ld[l] : (W2 >> l);
+        if ((shmask >> l & 1u) && pyr[l])
+            a.shadow[l] = shadow_offset((long long)B * H * W1, a.ld[l], pyr_dtype == RC_BF16 ? 2 : 4);
     }
     a.tiles_m = (W1 + 127) / 128;
     a.tiles_n = (W2 + 127) / 128;
@@ -117,6 +125,12 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
         rc = hip_rc(rc_launch_pool(pyr[l - 1], ldi, pyr[l], ldo, rows, W2 >> (l - 1), a.pyr_bf16, s),
                     "rc_corr_build: pool launch");
         if (rc) return rc;
+        if ((shmask >> l & 1u) && pyr[l]) {   // the same pooling step once more, into the level's shadow copy
+            void *sh = static_cast<char *>(pyr[l]) + shadow_offset(rows, ldo, a.pyr_bf16 ? 2 : 4);
+            rc = hip_rc(rc_launch_pool(pyr[l - 1], ldi, sh, ldo, rows, W2 >> (l - 1), a.pyr_bf16, s),
+                        "rc_corr_build: pool launch");
+            if (rc) return rc;
+        }
     }
     return RC_OK;
 }
@@ -124,6 +138,7 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
 extern "C" int rc_corr_pool(const void *in, long ld_in, void *out, long ld_out, long rows,
                             int W_in, int dtype, void *stream) {
     g_err[0] = 0;
+    dtype &= 0xFF;    // pools the primary copy; a shadow is not written
     if (rows < 0 || W_in < 2 || ld_in < W_in || ld_out < W_in / 2)
         return fail(RC_EINVAL, "rc_corr_pool: bad shape rows=%ld W_in=%d ld_in=%ld ld_out=%ld", rows,
                     W_in, ld_in, ld_out);
@@ -143,6 +158,8 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
                 long coord_batch_stride, int B, int H, int W1, const float *out, rc::LookupArgs &a,
                 bool *empty, bool allow_null = false) {
     *empty = false;
+    const unsigned shmask = ((unsigned)pyr_dtype >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits
+    pyr_dtype &= 0xFF;
     if (levels < 1 || levels > RC_MAX_LEVELS)
         return fail(RC_EINVAL, "%s: levels=%d outside 1..%d", who, levels, RC_MAX_LEVELS);
     if (radius < 1 || radius > 8)
@@ -176,6 +193,13 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
         if (a.ld[i] < widths[i])
             return fail(RC_EINVAL, "%s: level %d row stride %lld < width %d", who, i, a.ld[i],
                         widths[i]);
+        if (shmask >> i & 1u) {
+            const int es = pyr_dtype == RC_BF16 ? 2 : 4;
+            a.shadow[i] = shadow_offset(P, a.ld[i], es);
+            // the pair kernel addresses both copies with 32-bit buffer offsets
+            if (a.shadow[i] + P * a.ld[i] * es > 0xFFFFFF00LL)
+                return fail(RC_EUNSUPPORTED, "%s: level %d with its shadow copy exceeds 4 GiB", who, i);
+        }
     }
     a.coords = coords_x;
     a.cbs = coord_batch_stride;
@@ -239,6 +263,7 @@ extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, const l
     int rc = prep_lookup("rc_corr_lookup", pyr, widths, pyr_ld, pyr_dtype, levels, radius, coords_x,
                          coord_batch_stride, B, H, W1, out, a, &empty);
     if (rc || empty) return rc;
+    pyr_dtype &= 0xFF;
     a.out = out;
     return hip_rc(rc_launch_lookup(a, radius, pyr_dtype == RC_BF16,
                                    reinterpret_cast<hipStream_t>(stream)),
@@ -255,6 +280,7 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
     int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty, true);
     if (rc) return rc;
+    pyr_dtype &= 0xFF;
     bool pair;
     if ((rc = chain_kind("rc_corr_lookup_chain", pyr, widths, levels, radius, &pair))) return rc;
     if (pyr_dtype == RC_BF16 && !pair)
@@ -280,6 +306,7 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
     int rc = prep_lookup("rc_corr_lookup_step", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords1, 2L * H * W1, B, H, W1, out, a, &empty, chain != 0);
     if (rc || empty) return rc;
+    pyr_dtype &= 0xFF;
     if (!coords1_out || !flow_out)
         return fail(RC_EINVAL, "rc_corr_lookup_step: null coords1_out / flow_out");
     bool pair = false;
@@ -421,6 +448,7 @@ extern "C" int rc_corr_lookup_conv(const void *const *pyr, const int *widths, co
     int rc = prep_lookup("rc_corr_lookup_conv", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty);
     if (rc) return rc;
+    pyr_dtype &= 0xFF;
     if (levels < 2 || levels > 4 || radius > 4)
         return fail(RC_EUNSUPPORTED, "rc_corr_lookup_conv: levels 2..4 and radius 1..4 only");
     if (cout < 1) return fail(RC_EINVAL, "rc_corr_lookup_conv: cout=%d", cout);

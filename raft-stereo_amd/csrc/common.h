@@ -48,6 +48,14 @@ __device__ __forceinline__ float div_rn(float a, const DivRN &d) {
     return __builtin_fmaf(r, d.rb, q0);
 }
 
+// XCD-aware bijective block remap: hardware workgroup v runs on XCD v % 8, so
+// give XCD x the contiguous logical range [x*q + min(x, n%8), ...) of the n
+// blocks: neighbouring logical blocks then share an XCD (and its L2).
+__device__ __forceinline__ int xcd_remap(int v, int n) {
+    const int xcd = v & 7, q = n >> 3, rr = n & 7;
+    return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (v >> 3);
+}
+
 // Raw buffer resource over [base, base + bytes): loads past the end (or at a
 // "negative" offset, which wraps to a huge unsigned one) return 0 and never
 // fault.  Build it from wave-uniform values only (cdna_hip_programming.md T20).
@@ -92,6 +100,9 @@ struct BuildArgs {
     int pow2;                 // sqrt(D) is a power of two -> multiply is exact
     int pyr_bf16;             // store pyramid as bf16
     int stagger;              // dev-only: first-round stagger unit (s_sleep(127) count)
+    // line-phase shadow copies (ABI v5, RC_SHADOW): a stored level l is also
+    // written at (char*)lvl[l] + shadow[l] bytes (0 = no copy)
+    long long shadow[kMaxLevels];
 };
 
 struct LookupArgs {
@@ -113,6 +124,9 @@ struct LookupArgs {
     float *coords_out;
     float *flow_out;
     unsigned long long *dbg;  // dev library only: per-wave timeline stamps (else null)
+    // line-phase shadow copy of level i at (char*)lvl[i] + shadow[i] bytes
+    // (0 = none); read by the pair kernel (RC_SHADOW, ABI v5)
+    long long shadow[kMaxLevels];
 };
 
 // Backward of the lookup: level gradients (fp32, row stride ld[i] % 4 == 0).

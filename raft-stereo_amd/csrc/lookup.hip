@@ -470,7 +470,11 @@ __device__ __forceinline__ void tap_span(float xl, int W, int &f, int &l) {
     l = min((int)floorf(pb) + 1, W - 1);
 }
 
-template <int R, bool BF16 = false>
+// PH (dev-only timing probes; the values read are NOT the span's): 1 = read
+// each span at +64 B when that touches fewer 128-B lines (what a second,
+// half-line-shifted copy of the level would give), 2 = move every span to a
+// 128-B line start (lower bound: the fewest lines any layout could give).
+template <int R, bool BF16 = false, int PH = 0>
 __device__ __forceinline__ void issue_pair(PairSpan<R, BF16> &ps, const LookupArgs &a, int lo, float x,
                                            long long pblk, long long lrow) {
     typedef PairSpan<R, BF16> PS;
@@ -495,7 +499,27 @@ __device__ __forceinline__ void issue_pair(PairSpan<R, BF16> &ps, const LookupAr
     ps.sh = sa - ea;
     const long long ld = a.ld[lo];
     const char *lvl = static_cast<const char *>(a.lvl[lo]);
-    const auto rs = make_rsrc(lvl + pblk * ld * PS::ES, clamp_bytes((a.P - pblk) * ld * PS::ES));
+    // RC_SHADOW: the level also lies at +shb bytes, shifted by half a 128-B
+    // line; each lane reads its span from the copy in which it touches fewer
+    // lines (same values either way).  The resource then spans both copies.
+    const long long shb = a.shadow[lo];
+    const auto rs = make_rsrc(lvl + pblk * ld * PS::ES, clamp_bytes((a.P - pblk) * ld * PS::ES + shb));
+    uint32_t phase = 0;
+    if (shb != 0 || PH != 0) {
+        const unsigned long long b0 =
+            (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + (lo_e & ~(PS::EPC - 1))) * PS::ES);
+        const unsigned long long b1 = (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + hi_e) * PS::ES);
+        if (lo_e <= hi_e) {
+            if constexpr (PH == 2) {     // dev probe: line-aligned spans
+                phase = (uint32_t)((128 - (b0 & 127)) & 127);
+            } else {
+                const unsigned long long sh = PH == 1 ? 64ull : (unsigned long long)shb;
+                const long long l0 = (long long)(b1 >> 7) - (long long)(b0 >> 7);
+                const long long l1 = (long long)((b1 + sh) >> 7) - (long long)((b0 + sh) >> 7);
+                phase = l1 < l0 ? (uint32_t)sh : 0u;
+            }
+        }
+    }
 #pragma unroll
     for (int k = 0; k < PS::NC; ++k) {
         const int cs = ea + PS::EPC * k;
@@ -503,7 +527,7 @@ __device__ __forceinline__ void issue_pair(PairSpan<R, BF16> &ps, const LookupAr
         // ends inside its 16-B padded extent (ld % EPC == 0)
         const bool ok = cs <= hi_e && cs + PS::EPC - 1 >= lo_e;
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-            rs, ok ? (int)(uint32_t)((lrow * ld + cs) * PS::ES) : (int)0xFFFFFF00u, 0, 0);
+            rs, ok ? (int)((uint32_t)((lrow * ld + cs) * PS::ES) + phase) : (int)0xFFFFFF00u, 0, 0);
 #pragma unroll
         for (int c = 0; c < 4; ++c) ps.q[k][c] = v[c];
     }
@@ -658,16 +682,23 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
 // stores through a per-wave LDS tile (9 instead of 36 store instructions per
 // wave: 26.0 vs 25.8 us), two pixels per lane with both pixels' loads in
 // flight (26.6 us, 198 VGPRs).
-// M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-202, dev library):
-// 1 = no output stores, 2 = no fallback path.
+// M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-204, dev library):
+// 1 = no output stores, 2 = no fallback path, 3 / 4 = issue_pair's line-phase
+// probes PH 1 / 2 (timing only: wrong values), 5 = hardware block order
+// (no XCD remap; same values), 6 = PH 1.
 template <int R, int NL, int M = 0, bool BF16 = false>
 __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
     constexpr int NP = NL / 2;                        // spans per pixel
-    const PairPixel q = pair_pixel<R, NL>(a, (long long)blockIdx.x * 256);
+    // XCD-contiguous block order: neighbouring pixel blocks, whose output
+    // rows share 128-B lines at every channel plane's seams, run on one XCD
+    // (kitti B=64: 172 -> 166 us; config 2 unchanged; dev variant 205 = off)
+    const int blk = M == 5 ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+    const PairPixel q = pair_pixel<R, NL>(a, (long long)blk * 256);
     PairSpan<R, BF16> sp[NP];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
+    for (int k = 0; k < NP; ++k)
+        issue_pair<R, BF16, (M == 3 || M == 6) ? 1 : (M == 4 ? 2 : 0)>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
     auto sink = [&](int ch, float v) {
         if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
     };
@@ -733,9 +764,21 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
             hipLaunchKernelGGL((lookup_pair_stamped_kernel<R>), dim3(nblk), dim3(256), 0, s, a);
             return hipGetLastError();
         }
-        if (a.levels == 4 && (v == 201 || v == 202)) {
-            if (v == 201) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 202) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2>), dim3(nblk), dim3(256), 0, s, a);
+        if (a.levels == 4 && v >= 201 && v <= 206) {
+            if (v == 205 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 5>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 206 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 6>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 205 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 5, true>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 206 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 6, true>), dim3(nblk), dim3(256), 0, s, a);
+            // every variant in the pyramid's own element type (an fp32 kernel
+            // on a bf16 pyramid reads past the end of its buffers)
+            if (v == 201 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 202 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 201 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 202 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2, true>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 203 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 204 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 4>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 203 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3, true>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 204 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 4, true>), dim3(nblk), dim3(256), 0, s, a);
             return hipGetLastError();
         }
     }

@@ -52,7 +52,7 @@ constexpr int kStageFloats = 64 * 32;  // per-wave LDS staging: one 64x32 fp32 l
 
 // VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
 template <int VW>
-__device__ __forceinline__ void store_vec(void *lvl, bool bf16, long long g, const float *v) {
+__device__ __forceinline__ void store_vec1(void *lvl, bool bf16, long long g, const float *v) {
     if (bf16) {
         uint16_t *d = reinterpret_cast<uint16_t *>(lvl) + g;
         if constexpr (VW == 1) {
@@ -80,6 +80,14 @@ __device__ __forceinline__ void store_vec(void *lvl, bool bf16, long long g, con
     }
 }
 
+// ... and to the level's line-phase shadow copy at +sh bytes when sh != 0
+// (RC_SHADOW: the same values, every store duplicated; sh is wave-uniform).
+template <int VW>
+__device__ __forceinline__ void store_vec(void *lvl, bool bf16, long long g, const float *v, long long sh) {
+    store_vec1<VW>(lvl, bf16, g, v);
+    if (sh) store_vec1<VW>(static_cast<char *>(lvl) + sh, bf16, g, v);
+}
+
 // Store level l of a wave tile from its LDS staging image [FM*16 rows][cw =
 // 64>>l] as whole-row vector stores of VW elements per lane, 64/(cw/VW) rows
 // per wave instruction.  VW divides the row stride ld and the tile column
@@ -89,7 +97,7 @@ __device__ __forceinline__ void store_vec(void *lvl, bool bf16, long long g, con
 template <int FM, int VW>
 __device__ __forceinline__ void store_staged(const float *st, int l, void *lvl, long long ld,
                                              bool bf16, long long rowbase, int m0, int n0, int W1,
-                                             int Wl, int lane) {
+                                             int Wl, int lane, long long sh) {
     const int cw = 64 >> l;
     constexpr int lvw = VW == 8 ? 3 : (VW == 4 ? 2 : (VW == 2 ? 1 : 0));
     const int llpr = 6 - l - lvw;     // log2(lanes per row)
@@ -103,7 +111,7 @@ __device__ __forceinline__ void store_staged(const float *st, int l, void *lvl, 
             float v[VW];
 #pragma unroll
             for (int c = 0; c < VW; ++c) v[c] = st[R * cw + j + c];
-            store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v);
+            store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v, sh);
         }
     }
 }
@@ -111,16 +119,16 @@ __device__ __forceinline__ void store_staged(const float *st, int l, void *lvl, 
 template <int FM>
 __device__ __forceinline__ void store_staged_any(const float *st, int l, void *lvl, long long ld,
                                                  bool bf16, long long rowbase, int m0, int n0,
-                                                 int W1, int Wl, int lane) {
+                                                 int W1, int Wl, int lane, long long sh) {
     const int cw = 64 >> l;
     if (bf16 && ld % 8 == 0 && cw >= 8)
-        store_staged<FM, 8>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
+        store_staged<FM, 8>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane, sh);
     else if (ld % 4 == 0 && cw >= 4)
-        store_staged<FM, 4>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
+        store_staged<FM, 4>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane, sh);
     else if (ld % 2 == 0 && cw >= 2)
-        store_staged<FM, 2>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
+        store_staged<FM, 2>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane, sh);
     else
-        store_staged<FM, 1>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane);
+        store_staged<FM, 1>(st, l, lvl, ld, bf16, rowbase, m0, n0, W1, Wl, lane, sh);
 }
 
 template <int N>
@@ -232,11 +240,11 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
             // level 0: 4 consecutive w2 per lane, 16 lanes = one 64-wide row segment
             if (w1 < W1 && wb < W2) {
                 if (vec0) {
-                    store_vec<4>(a.lvl[0], bf, p * ld0 + wb, c);
+                    store_vec<4>(a.lvl[0], bf, p * ld0 + wb, c, a.shadow[0]);
                 } else {
 #pragma unroll
                     for (int nb = 0; nb < 4; ++nb)
-                        if (wb + nb < W2) store_vec<1>(a.lvl[0], bf, p * ld0 + wb + nb, &c[nb]);
+                        if (wb + nb < W2) store_vec<1>(a.lvl[0], bf, p * ld0 + wb + nb, &c[nb], a.shadow[0]);
                 }
             }
             if (a.nfused < 2) continue;
@@ -253,7 +261,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
         // read back from LDS in fp32: the same ops as avg_pool2d (:294)
         // (bf16 pyramid: of level l rounded to bf16, as stored).
         // a NULL level is computed (the next one needs it) but not stored
-        if (a.lvl[1]) store_staged_any<FM>(stA, 1, a.lvl[1], a.ld[1], bf, rowbase, m0, n0, W1, W2 >> 1, lane);
+        if (a.lvl[1]) store_staged_any<FM>(stA, 1, a.lvl[1], a.ld[1], bf, rowbase, m0, n0, W1, W2 >> 1, lane, a.shadow[1]);
         float *src = stA, *dst = stB;
         for (int l = 2; l < a.nfused; ++l) {
             const int cw = 64 >> l, cwp = 2 * cw;
@@ -264,7 +272,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
                 const float pm = (pr[0] + pr[1]) * 0.5f;
                 dst[R * cw + j] = bf ? round_bf16(pm) : pm;
             }
-            if (a.lvl[l]) store_staged_any<FM>(dst, l, a.lvl[l], a.ld[l], bf, rowbase, m0, n0, W1, W2 >> l, lane);
+            if (a.lvl[l]) store_staged_any<FM>(dst, l, a.lvl[l], a.ld[l], bf, rowbase, m0, n0, W1, W2 >> l, lane, a.shadow[l]);
             float *t = src;
             src = dst;
             dst = t;
@@ -649,7 +657,7 @@ __device__ __forceinline__ void lds_st1(uint32_t a, float v) {
 template <int VW>
 __device__ __forceinline__ void store_rows16(uint32_t st, int p, int cw, void *lvl, long long ld,
                                              bool bf16, long long rowbase, int w1_0, int col0, int W1,
-                                             int Wl, int lane) {
+                                             int Wl, int lane, long long sh) {
     const int lpr = cw / VW;                 // lanes per row
     const int rpi = 64 / lpr;                // rows per instruction
     const int Rl = lane / lpr, j = (lane - Rl * lpr) * VW;
@@ -679,23 +687,23 @@ __device__ __forceinline__ void store_rows16(uint32_t st, int p, int cw, void *l
             v[0] = x0;
         }
         const bool ok = Rl < rpi && R < 16 && w1 < W1 && col < Wl;
-        if (ok) store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v);
+        if (ok) store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v, sh);
     }
 }
 
 __device__ __forceinline__ void store_rows16_any(uint32_t st, int p, int cw, void *lvl, long long ld,
                                                  bool bf16, long long rowbase, int w1_0, int col0,
-                                                 int W1, int Wl, int lane) {
+                                                 int W1, int Wl, int lane, long long sh) {
     // widest vector dividing the image width (col0 is a multiple of it) and
     // the row stride
     if (bf16 && ld % 8 == 0 && cw % 8 == 0)
-        store_rows16<8>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
+        store_rows16<8>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
     else if (ld % 4 == 0 && cw % 4 == 0)
-        store_rows16<4>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
+        store_rows16<4>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
     else if (ld % 2 == 0 && cw % 2 == 0)
-        store_rows16<2>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
+        store_rows16<2>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
     else
-        store_rows16<1>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane);
+        store_rows16<1>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
 }
 
 __device__ __forceinline__ float pool2(float x, float y, bool bf) {
@@ -728,7 +736,7 @@ __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const Bui
         auto flush = [&](int l) {
             const int cw = WT >> l;
             store_rows16_any(st, cw + 4, cw, a.lvl[l], a.ld[l], bf, rowbase, m0 + 16 * nb, n0 >> l, a.W1,
-                             a.W2 >> l, lane);
+                             a.W2 >> l, lane, a.shadow[l]);
         };
         float v[FMA][4];
 #pragma unroll
@@ -1048,10 +1056,12 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             }
             // level 2 is small (8 B per lane and column): stored right away
             const int w1 = m0h + 16 * nb + i16, col = (n0h >> 2) + 4 * g;
-            if (!(MODE & kModeNoStores) && w1 < W1 && col < (W2 >> 2))
-                *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(a.lvl[2]) +
-                                           ((long long)row * W1 + w1) * a.ld[2] + col) =
-                    uint2{pack_bf16x2(qv[0], qv[1]), pack_bf16x2(qv[2], qv[3])};
+            if (!(MODE & kModeNoStores) && w1 < W1 && col < (W2 >> 2)) {
+                uint16_t *d = reinterpret_cast<uint16_t *>(a.lvl[2]) + ((long long)row * W1 + w1) * a.ld[2] + col;
+                const uint2 x = uint2{pack_bf16x2(qv[0], qv[1]), pack_bf16x2(qv[2], qv[3])};
+                *reinterpret_cast<uint2 *>(d) = x;
+                if (a.shadow[2]) *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(d) + a.shadow[2]) = x;
+            }
         }
     };
     // piece nb = level-0 rows 16nb..16nb+15 of the held tile: staged as bf16
@@ -1077,7 +1087,11 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             const int R = 8 * half + (ln >> 3), c = ln & 7;
             const uint4 x = *reinterpret_cast<const uint4 *>(img + R * 144 + 16 * c);
             const int w1 = hm0 + 16 * nb + R, col = hn0 + 8 * c;
-            if (w1 < W1 && col < W2) *reinterpret_cast<uint4 *>(l0 + (rowbase + w1) * a.ld[0] + col) = x;
+            if (w1 < W1 && col < W2) {
+                uint16_t *d = l0 + (rowbase + w1) * a.ld[0] + col;
+                *reinterpret_cast<uint4 *>(d) = x;
+                if (a.shadow[0]) *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(d) + a.shadow[0]) = x;
+            }
         }
     };
     auto zero_acc = [&]() {

@@ -73,17 +73,20 @@ def main():
     ap.add_argument("--dev-variants", default="",
                     help="RAFTCORR_LOOKUP_VARIANT values to time on the bench coords "
                          "(libraftcorr_dev.so)")
+    ap.add_argument("--only-dev", action="store_true",
+                    help="time only the dev variants, default kernel only")
     a = ap.parse_args()
     B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
     dev = torch.device("cuda", 0)
-    f1, f2, _ = bench.make_inputs(bench.CONFIGS[a.config], dev, seed=1)
+    dt = torch.bfloat16 if a.config in bench.BF16_CONFIGS else torch.float32
+    f1, f2, _ = bench.make_inputs(bench.CONFIGS[a.config], dev, seed=1, dtype=dt)
     P = B * H * W1
     lbytes = bench.lookup_bytes(P, L, r)
     res = {"config": a.config, "P": P, "alg_bytes": lbytes}
     with torch.no_grad():
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
         pyr = blk.corr_pyramid
-        for kind in ("bench", "same", "row", "smooth"):
+        for kind in (() if a.only_dev else ("bench", "same", "row", "smooth")):
             cs = coords_sets(B, H, W1, W2, iters, kind, dev)
             l1 = pyr[:2] + [None] * (L - 2)
             for name, fn in (("default", blk), ("chain_l1", lambda c: rcorr.lookup_chain(l1, c, L, r)),
@@ -98,8 +101,9 @@ def main():
             with _lib.dev_library():
                 for v in ["0"] + a.dev_variants.split(","):
                     os.environ["RAFTCORR_LOOKUP_VARIANT"] = v
-                    for name, fn in (("default", blk),
-                                     ("chain_l1", lambda c: rcorr.lookup_chain(l1, c, L, r))):
+                    fns = (("default", blk),) if a.only_dev else (
+                        ("default", blk), ("chain_l1", lambda c: rcorr.lookup_chain(l1, c, L, r)))
+                    for name, fn in fns:
                         us = time_seq(fn, cs, a.reps)
                         res[f"dev{v}/{name}"] = {"us": round(us, 2)}
             os.environ["RAFTCORR_LOOKUP_VARIANT"] = "0"

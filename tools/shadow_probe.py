@@ -1,0 +1,61 @@
+"""Which stored levels pay for an RC_SHADOW copy (dev probe).
+
+    python tools/shadow_probe.py [--config sceneflow|kitti] [--reps 5]
+
+For each shadow setting (none, level 0, level 2, both) the CorrBlock1D build
+and the 32 bench lookups are event-timed on the launch stream; prints build
+µs, median lookup µs and the corr-path step = build + iters x lookup.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from raft_stereo_amd import CorrBlock1D  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="sceneflow")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    cfg = bench.CONFIGS[a.config]
+    B, D, H, W1, W2, L, r, iters, _ = cfg
+    dev = torch.device("cuda", 0)
+    dt = torch.bfloat16 if a.config in bench.BF16_CONFIGS else torch.float32
+    f1, f2, coords = bench.make_inputs(cfg, dev, seed=1, dtype=dt)
+    res = {"config": a.config}
+    with torch.no_grad():
+        for name, sh in (("none", ()), ("l0", (0,)), ("l2", (2,)), ("l0+l2", (0, 2))):
+            bt, lt = [], []
+            for _ in range(a.reps):
+                torch.cuda._sleep(2_000_000)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, shadow=sh)
+                e1.record()
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+                ev[0].record()
+                for k in range(iters):
+                    blk(coords[k])
+                    ev[k + 1].record()
+                torch.cuda.synchronize()
+                assert blk._shadow == frozenset(sh)
+                bt.append(e0.elapsed_time(e1) * 1e3)
+                lt += [ev[k].elapsed_time(ev[k + 1]) * 1e3 for k in range(iters)]
+                del blk
+            bt.sort()
+            lt.sort()
+            b, l = bt[len(bt) // 2], lt[len(lt) // 2]
+            res[name] = {"build_us": round(b, 1), "lookup_us": round(l, 2),
+                         "step_us": round(b + iters * l, 1)}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
