@@ -494,7 +494,8 @@ class CorrBlock1D:
             pair = self._chain and num_levels in (2, 4) and lazy
             if shadow is None:
                 shadow = default_shadow_levels(B * H * W1, W2, num_levels, pyramid_dtype)
-            self._shadow = _shadow_levels(shadow, nbuf) if pair else frozenset()
+            self._shadow = (frozenset(l for l in _shadow_levels(shadow, nbuf) if l not in skip)
+                            if pair else frozenset())
             self._levels = build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype, skip=skip,
                                          shadow=self._shadow)
             self._levels += [None] * (num_levels + 1 - nbuf)
