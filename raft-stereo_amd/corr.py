@@ -95,6 +95,11 @@ def _prep_fmap(f):
     return f.contiguous()
 
 
+# Row stride granule of the stored levels (bytes): 16 keeps every store a
+# whole aligned vector.
+_ROW_ALIGN_BYTES = 16
+
+
 def _level_buffer(P, W, dtype, device, pad, shadow=False):
     """(P, 1, 1, W) tensor whose rows start 16-byte aligned: a view of a
     (P, ld) buffer with ld = W rounded up to 16 bytes when ``pad`` (the
@@ -102,7 +107,7 @@ def _level_buffer(P, W, dtype, device, pad, shadow=False):
     ``shadow``: the allocation also holds the level's RC_SHADOW copy at
     ``_lib.shadow_offset`` bytes (include/raftcorr.h); the view is the primary."""
     es = torch.tensor([], dtype=dtype).element_size()
-    per16 = 16 // es
+    per16 = _ROW_ALIGN_BYTES // es
     ld = -(-W // per16) * per16 if pad else W
     if shadow:
         total = _lib.shadow_offset(P, ld, es) + P * ld * es
@@ -132,7 +137,7 @@ def shadow_fits(P, W, dtype):
     """True when a level of width W and its RC_SHADOW copy fit the 4 GiB the
     pair kernel addresses with 32-bit buffer offsets."""
     es = torch.tensor([], dtype=dtype).element_size()
-    ld = -(-W // (16 // es)) * (16 // es)
+    ld = -(-W // (_ROW_ALIGN_BYTES // es)) * (_ROW_ALIGN_BYTES // es)
     return _lib.shadow_offset(P, ld, es) + P * ld * es <= 0xFFFFFF00
 
 

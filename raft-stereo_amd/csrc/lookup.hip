@@ -685,9 +685,10 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
 // M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-204, dev library):
 // 1 = no output stores, 2 = no fallback path, 3 / 4 = issue_pair's line-phase
 // probes PH 1 / 2 (timing only: wrong values), 5 = hardware block order
-// (no XCD remap; same values), 6 = PH 1.
-template <int R, int NL, int M = 0, bool BF16 = false>
-__global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
+// (no XCD remap; same values), 6 = PH 1, 7 = non-temporal output stores;
+// the WPE parameter (dev variants 208/209) caps registers for 5/6 waves/SIMD.
+template <int R, int NL, int M = 0, bool BF16 = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
     constexpr int NP = NL / 2;                        // spans per pixel
     // XCD-contiguous block order: neighbouring pixel blocks, whose output
@@ -700,7 +701,11 @@ __global__ __launch_bounds__(256) void lookup_pair_kernel(LookupArgs a) {
     for (int k = 0; k < NP; ++k)
         issue_pair<R, BF16, (M == 3 || M == 6) ? 1 : (M == 4 ? 2 : 0)>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
     auto sink = [&](int ch, float v) {
-        if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
+        if constexpr (M == 7) {               // dev: non-temporal output stores
+            if (q.active) __builtin_nontemporal_store(v, q.outp + (long long)ch * a.HW);
+        } else {
+            if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
+        }
     };
 #pragma unroll
     for (int k = 0; k < NP; ++k) finish_pair<R, M == 2, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink);
@@ -764,7 +769,14 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
             hipLaunchKernelGGL((lookup_pair_stamped_kernel<R>), dim3(nblk), dim3(256), 0, s, a);
             return hipGetLastError();
         }
-        if (a.levels == 4 && v >= 201 && v <= 206) {
+        if (a.levels == 4 && v >= 201 && v <= 209) {
+            // 208 / 209: at least 5 / 6 waves per SIMD (register cap)
+            if (v == 208 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 5>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 208 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 5>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 209 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 6>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 209 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 6>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 207 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 7>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 207 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 7, true>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 205 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 5>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 206 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 6>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 205 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 5, true>), dim3(nblk), dim3(256), 0, s, a);

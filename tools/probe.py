@@ -39,7 +39,8 @@ def main():
         big = torch.randn(1 << 28, device=dev)
         cal = big.clone()   # calibration: 1 GiB read + 1 GiB write
         del cal
-        f1, f2, coords = bench.make_inputs(cfg, dev, seed=1)
+        # a bf16 pyramid comes from bf16 fmaps, as in bench.py (the ring kernel)
+        f1, f2, coords = bench.make_inputs(cfg, dev, seed=1, dtype=pdt)
         blk = None
         for _ in range(a.iters):
             blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=pdt)

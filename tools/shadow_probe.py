@@ -23,15 +23,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="sceneflow")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--row-align", type=int, default=16,
+                    help="row stride granule of the stored levels in bytes (corr._ROW_ALIGN_BYTES)")
+    ap.add_argument("--settings", default="none,l0,l2,l0+l2")
     a = ap.parse_args()
+    from raft_stereo_amd import corr as rcorr
+    rcorr._ROW_ALIGN_BYTES = a.row_align
     cfg = bench.CONFIGS[a.config]
     B, D, H, W1, W2, L, r, iters, _ = cfg
     dev = torch.device("cuda", 0)
     dt = torch.bfloat16 if a.config in bench.BF16_CONFIGS else torch.float32
     f1, f2, coords = bench.make_inputs(cfg, dev, seed=1, dtype=dt)
-    res = {"config": a.config}
+    res = {"config": a.config, "row_align": a.row_align}
+    want = set(a.settings.split(","))
     with torch.no_grad():
         for name, sh in (("none", ()), ("l0", (0,)), ("l2", (2,)), ("l0+l2", (0, 2))):
+            if name not in want:
+                continue
             bt, lt = [], []
             for _ in range(a.reps):
                 torch.cuda._sleep(2_000_000)
