@@ -16,7 +16,7 @@ way, exchanging only the GRU state halos each iteration.
 import torch
 import torch.distributed as dist
 
-from .corr import CorrBlock1D
+from .corr import CorrBlock1D, coords_grid
 
 
 def _host_staged(t, group=None):
@@ -105,13 +105,53 @@ def _interp_rows(x, src_lo, src_glob, dst_lo, dst_hi, dst_glob, dst_w):
                                            align_corners=True)
 
 
+def _all_reduce_sum(t, group=None):
+    """In-place SUM all-reduce (host-staged for gloo on CUDA tensors)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return t
+    if _host_staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+    return t
+
+
+def _instance_norm_rows(y, lo, hi, group, eps):
+    """nn.InstanceNorm2d (affine=False, model.py:35-39 'instance') of a row
+    SLAB with the statistics of the WHOLE image: every rank sums x and x^2
+    over its owned rows [lo, hi) (the owned rows of all ranks partition the
+    image), one all-reduce of 2*N*C+1 doubles, then the biased mean/var of
+    the image normalise every slab row (halo rows included)."""
+    yo = y[:, :, lo:hi].double()
+    N, C = y.shape[:2]
+    st = torch.cat([yo.sum((2, 3)).reshape(-1), (yo * yo).sum((2, 3)).reshape(-1),
+                    torch.tensor([float((hi - lo) * y.shape[3])], dtype=torch.float64, device=y.device)])
+    _all_reduce_sum(st, group)
+    n = st[-1]
+    mean = st[:N * C] / n
+    var = (st[N * C:2 * N * C] / n - mean * mean).clamp_min(0)
+    inv = torch.rsqrt(var + eps)
+    # fp32 out, as InstanceNorm under autocast
+    return (y.float() - mean.view(N, C, 1, 1).float()) * inv.view(N, C, 1, 1).float()
+
+
 class RowShardedStereo:
     """Row-sharded RAFT-Stereo forward over ``world`` ranks (one per GPU).
 
-    * Encoders (cnet, conv2, context convs) run replicated on the full image,
-      so conv2's InstanceNorm statistics (model.py:35-39, :345) need no
-      exchange (SURVEY.md §8e item 1 sidestepped at the cost of redundant
-      encoder FLOPs).
+    * Encoders (``shard_encoders=True``, default):
+      each rank runs cnet, conv2 and the context convs on its own band of
+      image rows -- its GRU slab (below) plus ``enc_margin`` rows at 1/f res
+      on either side, which cover the encoders' receptive field (the
+      1/16-res heads and context convs reach past 128 full-res rows at
+      f = 4: 32 rows left the slab's edge row at 1/16 res off by 4e-4, 48
+      make every slab row equal to the full-image features), so the slab's
+      features equal the full-image ones.  cnet's BatchNorms run on running stats in
+      eval mode (per pixel); conv2's two InstanceNorms (model.py:35-39, :345)
+      take image-wide statistics through one all-reduce each
+      (``_instance_norm_rows``).  ``shard_encoders=False`` runs the encoders
+      replicated on the full image (no exchange; redundant encoder FLOPs).
     * Rank k owns 1/4-res feature rows [r0, r1) (multiples of 4) and keeps GRU
       state for the extended slab [r0 - halo, r1 + halo) (1/8 and 1/16 res:
       halo/2, halo/4).  The correlation pyramid is built for the slab's rows
@@ -125,10 +165,13 @@ class RowShardedStereo:
       ``gather_rows`` assembles full-height tensors.
     """
 
-    def __init__(self, model, rank, world, halo=32, group=None):
+    def __init__(self, model, rank, world, halo=32, group=None, shard_encoders=True, enc_margin=48):
         if halo % 4:
             raise ValueError("halo must be a multiple of 4")
+        if enc_margin % 4:
+            raise ValueError("enc_margin must be a multiple of 4")
         self.model, self.rank, self.world, self.halo, self.group = model, rank, world, halo, group
+        self.shard_encoders, self.enc_margin = shard_encoders, enc_margin
 
     # row geometry -----------------------------------------------------------
     def _ranges(self, H1):
@@ -185,22 +228,82 @@ class RowShardedStereo:
                 t[:, :, at:at + buf.shape[2]] = buf
         return t.to(dev) if staged else t
 
+    # encoders ---------------------------------------------------------------
+    @staticmethod
+    def _heights(H, n_down, nl):
+        """Global row counts of the 1/f, 1/2f, 1/4f feature levels for an image
+        of H rows (each stride-2 3x3 conv with padding 1 maps h -> ceil(h/2))."""
+        h = H
+        for _ in range(n_down):
+            h = (h + 1) // 2
+        glob = [h]
+        for _ in range(1, nl):
+            glob.append((glob[-1] + 1) // 2)
+        return glob
+
+    def _features_rows(self, image1, image2, e0, e1, r0, r1):
+        """RAFTStereo.features (model.py:339-364) on a band of image rows.
+        Returns the slab [e0, e1) of fmap1/fmap2 (1/f res) and of every GRU
+        level's net / inp tensors -- equal to slicing the full-image features."""
+        m, a = self.model, self.model.args
+        if m.training:
+            raise RuntimeError("RowShardedStereo: encoder row sharding needs eval mode "
+                               "(BatchNorm running statistics)")
+        f = 2 ** a.n_downsample
+        H = image1.shape[2]
+        mg = self.enc_margin
+        # band of 1/f rows [b0, b1): start a multiple of 4 (the 1/4f heads'
+        # stride), so every strided conv of the band samples the global grid
+        b0 = max(0, e0 - mg)
+        b1 = min(-(-H // f), e1 + mg)
+        s0, s1 = f * b0, min(H, f * b1)
+        i1 = (2 * (image1[:, :, s0:s1] / 255.0) - 1.0).contiguous()
+        i2 = (2 * (image2[:, :, s0:s1] / 255.0) - 1.0).contiguous()
+        n = a.n_gru_layers
+        with m._autocast():
+            *cnet_list, x = m.cnet(torch.cat((i1, i2), dim=0), dual_inp=True, num_layers=n)
+            blk, conv = m.conv2[0], m.conv2[1]
+            lo, hi = r0 - b0, r1 - b0                      # owned rows, band-local
+            eps = blk.norm1.eps
+            y = blk.relu(_instance_norm_rows(blk.conv1(x), lo, hi, self.group, eps))
+            y = blk.relu(_instance_norm_rows(blk.conv2(y), lo, hi, self.group, eps))
+            fm = conv(x + y)
+            fmap1, fmap2 = fm.split(dim=0, split_size=x.shape[0] // 2)
+            net_list = [torch.tanh(pair[0]) for pair in cnet_list]
+            inp_list = [torch.relu(pair[1]) for pair in cnet_list]
+            inp_list = [list(c(i).split(dim=1, split_size=c.out_channels // 3))
+                        for i, c in zip(inp_list, m.context_zqr_convs)]
+        sl = slice(e0 - b0, e1 - b0)
+        ext = [self._lvl(e0, e1, l) for l in range(n)]
+        bl = [b0 >> l for l in range(n)]
+        net = [net_list[l][:, :, ext[l][0] - bl[l]:ext[l][1] - bl[l]] for l in range(n)]
+        inp = [[c[:, :, ext[l][0] - bl[l]:ext[l][1] - bl[l]] for c in inp_list[l]] for l in range(n)]
+        return fmap1[:, :, sl], fmap2[:, :, sl], net, inp
+
     # forward ----------------------------------------------------------------
     def forward(self, image1, image2, iters=12):
         m, a = self.model, self.model.args
-        fmap1, fmap2, net_full, inp_full = m.features(image1, image2)
-        H1 = fmap1.shape[2]
-        r0, r1, e0, e1 = self._ranges(H1)
-        nl = len(net_full)
+        nl = a.n_gru_layers
+        if self.shard_encoders:
+            glob = self._heights(image1.shape[2], a.n_downsample, nl)
+            H1 = glob[0]
+            r0, r1, e0, e1 = self._ranges(H1)
+            fmap1, fmap2, net, inp = self._features_rows(image1, image2, e0, e1, r0, r1)
+        else:
+            fmap1, fmap2, net_full, inp_full = m.features(image1, image2)
+            H1 = fmap1.shape[2]
+            r0, r1, e0, e1 = self._ranges(H1)
+            glob = [t.shape[2] for t in net_full]
+            ext0 = [self._lvl(e0, e1, l) for l in range(nl)]
+            net = [net_full[l][:, :, ext0[l][0]:ext0[l][1]] for l in range(nl)]
+            inp = [[c[:, :, ext0[l][0]:ext0[l][1]] for c in inp_full[l]] for l in range(nl)]
+            fmap1, fmap2 = fmap1[:, :, e0:e1], fmap2[:, :, e0:e1]
         own = [self._lvl(r0, r1, l) for l in range(nl)]
         ext = [self._lvl(e0, e1, l) for l in range(nl)]
-        glob = [t.shape[2] for t in net_full]
-        net = [net_full[l][:, :, ext[l][0]:ext[l][1]] for l in range(nl)]
-        inp = [[c[:, :, ext[l][0]:ext[l][1]] for c in inp_full[l]] for l in range(nl)]
-        corr_fn = m.corr_block(fmap1[:, :, e0:e1].contiguous(), fmap2[:, :, e0:e1].contiguous(),
+        corr_fn = m.corr_block(fmap1.contiguous(), fmap2.contiguous(),
                                radius=a.corr_radius, num_levels=a.corr_levels)
         B, _, _, W1 = fmap1.shape
-        coords0 = m.initialize_flow(net_full[0])[0][:, :, e0:e1]
+        coords0 = coords_grid(B, H1, W1).to(fmap1.device)[:, :, e0:e1]
         coords1 = coords0.clone()
         blk = m.update_block
         n = a.n_gru_layers

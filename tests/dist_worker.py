@@ -70,7 +70,7 @@ def run(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4):
+def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders=True):
     """Row-sharded network forward vs the unsharded one (oracle corr block)."""
     import torch
     import torch.distributed as dist
@@ -86,12 +86,52 @@ def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4):
         img1 = torch.rand(1, 3, H, W, generator=g) * 255
         img2 = torch.roll(img1, -4, dims=-1)
         net = model()
-        rs = RowShardedStereo(net, rank, world, halo=halo)
+        rs = RowShardedStereo(net, rank, world, halo=halo, shard_encoders=shard_encoders)
         with torch.no_grad():
             preds = rs.forward(img1, img2, iters=iters)
             full = [rs.gather_rows(p) for p in preds]
         q.put((rank, torch.stack(full), None))
     except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_features(rank, world, port, q, halo=24, H=800, W=64):
+    """Row-sharded encoders (band of image rows + InstanceNorm all-reduce)
+    vs the full-image encoders sliced to this rank's GRU slab: max |diff|
+    over fmap1, fmap2 and every level's net / inp tensors, and the band's
+    1/f row range (to show the band did not cover the whole image)."""
+    import torch
+    import torch.distributed as dist
+    import pkgload
+    pkgload.load()
+    from raft_stereo_amd.shard import RowShardedStereo
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    try:
+        g = torch.Generator().manual_seed(11)
+        img1 = torch.rand(1, 3, H, W, generator=g) * 255
+        img2 = torch.roll(img1, -3, dims=-1)
+        net = model()
+        rs = RowShardedStereo(net, rank, world, halo=halo)
+        with torch.no_grad():
+            f1, f2, nf, inf = net.features(img1, img2)
+            H1 = f1.shape[2]
+            r0, r1, e0, e1 = rs._ranges(H1)
+            s1, s2, ns, ins = rs._features_rows(img1, img2, e0, e1, r0, r1)
+            d = max((s1 - f1[:, :, e0:e1]).abs().max().item(), (s2 - f2[:, :, e0:e1]).abs().max().item())
+            for l in range(len(nf)):
+                lo, hi = rs._lvl(e0, e1, l)
+                d = max(d, (ns[l] - nf[l][:, :, lo:hi]).abs().max().item())
+                for a, b in zip(ins[l], inf[l]):
+                    d = max(d, (a - b[:, :, lo:hi]).abs().max().item())
+        band = (max(0, e0 - rs.enc_margin), min(H1, e1 + rs.enc_margin))
+        q.put((rank, d, (H1, band)))
+    except Exception:
         import traceback
         q.put((rank, traceback.format_exc(), None))
     finally:

@@ -75,15 +75,19 @@ def test_gloo_world2_batch_and_row_sharding():
     assert torch.equal(res[0][1], torch_ref.TorchCorrBlock1D(f1, f2, 3, 3)(coords))
 
 
-@pytest.mark.parametrize("world,halo", [(2, 32), (3, 24)])
-def test_gloo_row_sharded_network(world, halo):
+@pytest.mark.parametrize("world,halo,H,W,shard_enc", [(2, 32, 320, 96, False), (3, 24, 320, 96, True),
+                                                       (2, 32, 800, 64, True)])
+def test_gloo_row_sharded_network(world, halo, H, W, shard_enc):
     """Full network row-sharded over ``world`` ranks (GRU halo exchange by
     point-to-point send/recv each iteration) == unsharded forward.  H=320 ->
     80 feature rows: 40/40 rows with a 32-row halo, 28/28/24 with 24.  A halo
     that covers the one-iteration cone (<= 20 rows) is exact to
-    rounding (measured 3.8e-6 px max); 8 rows gives 1.3e-4, 4 rows 6e-3."""
-    H, W, iters = 320, 96, 4
-    res = _spawn(dist_worker.run_rows, world, halo, H, W, iters)
+    rounding (measured 3.8e-6 px max); 8 rows gives 1.3e-4, 4 rows 6e-3.
+    ``shard_enc``: the encoders run on each rank's band of image rows with
+    all-reduced InstanceNorm statistics (H=800: the bands do not cover the
+    image) instead of replicated on the full image."""
+    iters = 4
+    res = _spawn(dist_worker.run_rows, world, halo, H, W, iters, shard_enc)
     g = torch.Generator().manual_seed(3)
     img1 = torch.rand(1, 3, H, W, generator=g) * 255
     img2 = torch.roll(img1, -4, dims=-1)
@@ -94,3 +98,17 @@ def test_gloo_row_sharded_network(world, halo):
         assert got.shape == ref.shape
         assert (got - ref).abs().max() < 5e-5, (got - ref).abs().max()
         assert (got - ref).abs().mean() < 1e-6
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_row_sharded_encoders_match_full(world):
+    """each rank's encoder band (its GRU slab + 48
+    rows of 1/f margin) with conv2's InstanceNorm statistics all-reduced
+    gives the full-image features on the slab, to fp32 rounding of the
+    statistics (sums in fp64 vs PyTorch's fp32 reduction)."""
+    res = _spawn(dist_worker.run_features, world, 24, 800, 64)
+    H1 = res[0][1][0]
+    for r in range(world):
+        assert res[r][0] < 2e-5, (r, res[r][0])
+    # the bands are proper sub-ranges: encoders really ran on part of the image
+    assert any(b != (0, H1) for _, (_, b) in ((r, res[r][1]) for r in range(world)))

@@ -3,17 +3,22 @@ the row-sharded forward, timed separately, and the scaling cap they imply.
 
     python tools/shard_probe.py [--iters 32] [--halo 32]
 
-shard.RowShardedStereo runs the encoders (cnet + conv2 + context convs,
-model.py:359-365) REPLICATED on the full image on every rank and shards only
-the per-iteration work (corr lookup + GRU update, model.py:374-383) by rows
-of the 1/4-resolution grid, each rank keeping a +-halo slab.  Timed here:
-  E    = RAFTStereo.features on the full image (every rank pays it);
+shard.RowShardedStereo shards the per-iteration work (corr lookup + GRU
+update, model.py:374-383) by rows of the 1/4-resolution grid, each rank
+keeping a +-halo slab, and either runs the encoders (cnet + conv2 + context
+convs, model.py:359-365) replicated on the full image or (default) on a band
+of image rows around its slab (``shard_encoders``).  Timed here:
+  E    = RAFTStereo.features on the full image (the replicated encoders);
+  Es(N)= the encoders on the widest rank's band (a middle rank: slab +
+         2 x enc_margin rows; the one InstanceNorm all-reduce of each of
+         conv2's two norms is not included -- a few KB);
   C(n) = the corr build of an n-row slab;
   U(n) = one iteration on an n-row slab: lookup + update block (with the
          slab-local interp of RowShardedStereo._gru), n = H1/N + 2*halo;
 then T(N) = E + C(n_N) + iters * U(n_N) (halo exchange not included: a few
 MB per neighbour per iteration over xGMI, tens of us) and the speedup
-T(1) / T(N).  The replicated encoder bounds it: T(N) >= E.
+T(1) / T(N).  The replicated encoder bounds it: T(N) >= E; with sharded
+encoders Ts(N) = Es(N) + C(n_N) + iters * U(n_N).
 """
 import argparse
 import json
@@ -88,12 +93,21 @@ def main():
                                           align_corners=True), True, True, True)
             U = timed(one_iter)
             T = E + C + a.iters * U
+            if N > 1:   # a middle rank's band (single process: no all-reduce)
+                rm = RowShardedStereo(model, N // 2, N, halo=a.halo)
+                q0, q1, x0, x1 = rm._ranges(H1)
+                Es = timed(lambda: rm._features_rows(img1, img2, x0, x1, q0, q1))
+                band = min(H1, x1 + rm.enc_margin) - max(0, x0 - rm.enc_margin)
+            else:
+                Es, band = E, H1
             out[N] = {"slab_rows": n, "C_build_ms": C * 1e3, "U_iter_ms": U * 1e3,
-                      "T_ms": T * 1e3}
+                      "T_ms": T * 1e3, "Es_band_ms": Es * 1e3, "band_rows": band,
+                      "Ts_sharded_ms": (Es + C + a.iters * U) * 1e3}
         T1 = out[1]["T_ms"]
         for N in out:
             out[N]["speedup"] = T1 / out[N]["T_ms"]
             out[N]["encoder_share"] = res["E_encoders_ms"] / out[N]["T_ms"]
+            out[N]["speedup_sharded"] = T1 / out[N]["Ts_sharded_ms"]
         res["per_N"] = out
         res["amdahl_cap"] = T1 / res["E_encoders_ms"]
     print(json.dumps(res, indent=1))
