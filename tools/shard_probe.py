@@ -69,6 +69,7 @@ def main():
         fmap1, fmap2, net, inp = model.features(img1, img2)
         H1 = fmap1.shape[2]
         res["E_encoders_ms"] = E * 1e3
+        print(f"E = {E * 1e3:.1f} ms", flush=True)
         blk = model.update_block
         out = {}
         for N in (1, 2, 4, 8):
@@ -103,6 +104,7 @@ def main():
             out[N] = {"slab_rows": n, "C_build_ms": C * 1e3, "U_iter_ms": U * 1e3,
                       "T_ms": T * 1e3, "Es_band_ms": Es * 1e3, "band_rows": band,
                       "Ts_sharded_ms": (Es + C + a.iters * U) * 1e3}
+            print(f"N={N}: {json.dumps(out[N])}", flush=True)   # progress (long run)
         T1 = out[1]["T_ms"]
         for N in out:
             out[N]["speedup"] = T1 / out[N]["T_ms"]
