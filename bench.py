@@ -518,14 +518,14 @@ def main():
                        "algorithmic_bytes": vbytes, "flops": vflops,
                        "kernel": ("rc::build_bf16_ring_kernel" if W2 > 64 else "rc::build_bf16_kernel"),
                        "avg_launch_us": build_ms * 1e3,
-                       "levels_written": written}
+                       "levels_written": written, "shadow_levels": sorted(blk._shadow)}
     else:
         roof_volume = {"bound": "mfma", "achieved": vflops / (build_ms * 1e-3) / 1e12,
                        "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                        "frac": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
                        "traffic": traffic.get("build_bytes"), "algorithmic_bytes": vbytes,
                        "kernel": "rc::build_f32_ring_kernel<4,0>", "avg_launch_us": build_ms * 1e3,
-                       "levels_written": written}
+                       "levels_written": written, "shadow_levels": sorted(blk._shadow)}
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     pair = blk._chain and (L == 2 or (L == 4 and 2 in written))
     lname = (f"rc::lookup_pair_kernel<{r},{L}>" if pair else
@@ -575,7 +575,9 @@ def main():
         "kernel_ms": {"build": build_ms, "lookup_in_loop": lookup_ms,
                       "lookup_per_launch": lookup_launch_ms},
         "cpu_baseline": None,
-        "notes": (f"fp32 blocks: the build writes pyramid levels {written}; every lookup "
+        "notes": (f"pool-chain block: the build writes pyramid levels {written} (levels "
+                  f"{sorted(blk._shadow)} also as a half-line-shifted RC_SHADOW copy: those "
+                  "writes are in the build's time, not in its algorithmic bytes); every lookup "
                   "recomputes the others from them bit-exactly (rc_corr_lookup_chain); the rest "
                   "are materialised only when corr_pyramid is read" if blk._chain else
                   "the build writes all num_levels+1 pyramid levels"),
