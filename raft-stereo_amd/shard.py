@@ -156,22 +156,28 @@ class RowShardedStereo:
       state for the extended slab [r0 - halo, r1 + halo) (1/8 and 1/16 res:
       halo/2, halo/4).  The correlation pyramid is built for the slab's rows
       only -- the corr path is row-local (model.py:324, :299/:308).
-    * One iteration on the slab is exact on the owned rows when ``halo``
-      covers the one-iteration dependency cone (<= 20 rows, SURVEY.md §8e);
-      afterwards the owned boundary rows of net[0..2] and coords1 are sent to
-      the two neighbours with point-to-point send/recv (RCCL over xGMI on the
-      GPU box), refreshing their halos.
+    * Halo exchange (default ``per_stage=True``): the owned
+      boundary rows of net[2] go to the two neighbours right after gru32, of
+      net[1] after gru16, and of net[0] and coords1 at the end of the
+      iteration (point-to-point send/recv: RCCL over xGMI on the GPU box), so
+      the halo only has to cover one stage's dependency cone: 12 rows at 1/4
+      res are exact to rounding (gloo, 3 ranks: 1.9e-6 px max; 8 rows
+      5.7e-6; 4 rows 8.8e-3).  ``per_stage=False`` exchanges every level once
+      per iteration and needs a halo covering the whole iteration's cone
+      (<= 20 rows; 24-32 used).
     * ``forward`` returns the per-iteration flow of the OWNED rows;
       ``gather_rows`` assembles full-height tensors.
     """
 
-    def __init__(self, model, rank, world, halo=32, group=None, shard_encoders=True, enc_margin=48):
+    def __init__(self, model, rank, world, halo=12, group=None, shard_encoders=True, enc_margin=48,
+                 per_stage=True):
         if halo % 4:
             raise ValueError("halo must be a multiple of 4")
         if enc_margin % 4:
             raise ValueError("enc_margin must be a multiple of 4")
         self.model, self.rank, self.world, self.halo, self.group = model, rank, world, halo, group
         self.shard_encoders, self.enc_margin = shard_encoders, enc_margin
+        self.per_stage = per_stage
 
     # row geometry -----------------------------------------------------------
     def _ranges(self, H1):
@@ -312,35 +318,45 @@ class RowShardedStereo:
             return _interp_rows(x, ext[ls][0], glob[ls], ext[ld][0], ext[ld][1], glob[ld],
                                 net[ld].shape[3])
 
+        # per_stage: refresh net[2] after gru32 and net[1] after gru16 as well
+        # (the exchange per stage), so the halo only has to cover
+        # one stage's cone instead of a whole iteration's
+        xch = ((lambda t, l: self._exchange(t, l, own[l], ext[l], glob[l])) if self.per_stage
+               else None)
         preds = []
         for _ in range(iters):
             corr = corr_fn(coords1)
             flow = coords1 - coords0
             with m._autocast():
                 if n == 3 and a.slow_fast_gru:
-                    self._gru(blk, net, inp, None, None, interp, True, False, False)
+                    self._gru(blk, net, inp, None, None, interp, True, False, False, xch)
                 if n >= 2 and a.slow_fast_gru:
-                    self._gru(blk, net, inp, None, None, interp, n == 3, True, False)
-                delta = self._gru(blk, net, inp, corr, flow, interp, n == 3, n >= 2, True)
+                    self._gru(blk, net, inp, None, None, interp, n == 3, True, False, xch)
+                delta = self._gru(blk, net, inp, corr, flow, interp, n == 3, n >= 2, True, xch)
             delta[:, 1] = 0.0
             coords1 = coords1 + delta.float()
             preds.append((coords1 - coords0)[:, :, r0 - e0:r1 - e0])
-            for l in range(nl):
+            for l in range(1 if self.per_stage else nl):
                 net[l] = self._exchange(net[l], l, own[l], ext[l], glob[l])
             coords1 = self._exchange(coords1, 0, own[0], ext[0], glob[0])
         return preds
 
     @staticmethod
-    def _gru(blk, net, inp, corr, flow, interp, iter32, iter16, iter08):
+    def _gru(blk, net, inp, corr, flow, interp, iter32, iter16, iter08, xch=None):
         """BasicMultiUpdateBlock.forward (model.py:242-265) on a slab, with the
-        global-row interp; returns delta_flow when iter08."""
+        global-row interp; returns delta_flow when iter08.  ``xch(t, level)``
+        (per-stage mode) refreshes a level's halo rows after its update."""
         from .network import pool2x
         n = blk.args.n_gru_layers
         if iter32:
             net[2] = blk.gru32(net[2], *inp[2], pool2x(net[1]))
+            if xch is not None:
+                net[2] = xch(net[2], 2)
         if iter16:
             extra = (interp(net[2], 2, 1),) if n > 2 else ()
             net[1] = blk.gru16(net[1], *inp[1], pool2x(net[0]), *extra)
+            if xch is not None:
+                net[1] = xch(net[1], 1)
         if iter08:
             motion = blk.encoder(flow, corr)
             extra = (interp(net[1], 1, 0),) if n > 1 else ()

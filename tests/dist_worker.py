@@ -70,7 +70,8 @@ def run(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders=True):
+def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders=True,
+             per_stage=False):
     """Row-sharded network forward vs the unsharded one (oracle corr block)."""
     import torch
     import torch.distributed as dist
@@ -86,7 +87,8 @@ def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders
         img1 = torch.rand(1, 3, H, W, generator=g) * 255
         img2 = torch.roll(img1, -4, dims=-1)
         net = model()
-        rs = RowShardedStereo(net, rank, world, halo=halo, shard_encoders=shard_encoders)
+        rs = RowShardedStereo(net, rank, world, halo=halo, shard_encoders=shard_encoders,
+                              per_stage=per_stage)
         with torch.no_grad():
             preds = rs.forward(img1, img2, iters=iters)
             full = [rs.gather_rows(p) for p in preds]

@@ -75,9 +75,10 @@ def test_gloo_world2_batch_and_row_sharding():
     assert torch.equal(res[0][1], torch_ref.TorchCorrBlock1D(f1, f2, 3, 3)(coords))
 
 
-@pytest.mark.parametrize("world,halo,H,W,shard_enc", [(2, 32, 320, 96, False), (3, 24, 320, 96, True),
-                                                       (2, 32, 800, 64, True)])
-def test_gloo_row_sharded_network(world, halo, H, W, shard_enc):
+@pytest.mark.parametrize("world,halo,H,W,shard_enc,per_stage", [
+    (2, 32, 320, 96, False, False), (3, 24, 320, 96, True, False),
+    (3, 12, 320, 96, True, True), (2, 12, 800, 64, True, True)])
+def test_gloo_row_sharded_network(world, halo, H, W, shard_enc, per_stage):
     """Full network row-sharded over ``world`` ranks (GRU halo exchange by
     point-to-point send/recv each iteration) == unsharded forward.  H=320 ->
     80 feature rows: 40/40 rows with a 32-row halo, 28/28/24 with 24.  A halo
@@ -85,9 +86,10 @@ def test_gloo_row_sharded_network(world, halo, H, W, shard_enc):
     rounding (measured 3.8e-6 px max); 8 rows gives 1.3e-4, 4 rows 6e-3.
     ``shard_enc``: the encoders run on each rank's band of image rows with
     all-reduced InstanceNorm statistics (H=800: the bands do not cover the
-    image) instead of replicated on the full image."""
+    image) instead of replicated on the full image.  ``per_stage``: halos
+    refreshed after each GRU stage, so 12 rows suffice (the default)."""
     iters = 4
-    res = _spawn(dist_worker.run_rows, world, halo, H, W, iters, shard_enc)
+    res = _spawn(dist_worker.run_rows, world, halo, H, W, iters, shard_enc, per_stage)
     g = torch.Generator().manual_seed(3)
     img1 = torch.rand(1, 3, H, W, generator=g) * 255
     img2 = torch.roll(img1, -4, dims=-1)

@@ -1,7 +1,7 @@
 """Config 4 (Middlebury 1984x2880, bs=1, 32 iters) on ONE GPU: the pieces of
 the row-sharded forward, timed separately, and the scaling cap they imply.
 
-    python tools/shard_probe.py [--iters 32] [--halo 32]
+    python tools/shard_probe.py [--iters 32] [--halo 12]
 
 shard.RowShardedStereo shards the per-iteration work (corr lookup + GRU
 update, model.py:374-383) by rows of the 1/4-resolution grid, each rank
@@ -53,7 +53,8 @@ def timed(fn, reps=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=32)
-    ap.add_argument("--halo", type=int, default=32)
+    ap.add_argument("--halo", type=int, default=12,
+                    help="1/4-res halo rows (12: per-stage exchange, the default; 32: once per iteration)")
     ap.add_argument("--H", type=int, default=1984)
     ap.add_argument("--W", type=int, default=2880)
     a = ap.parse_args()
