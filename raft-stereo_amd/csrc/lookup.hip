@@ -686,7 +686,8 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
 // 1 = no output stores, 2 = no fallback path, 3 / 4 = issue_pair's line-phase
 // probes PH 1 / 2 (timing only: wrong values), 5 = hardware block order
 // (no XCD remap; same values), 6 = PH 1, 7 = non-temporal output stores;
-// the WPE parameter (dev variants 208/209) caps registers for 5/6 waves/SIMD.
+// the WPE parameter (dev variants 208/209) caps registers for 5/6 waves/SIMD;
+// 9 (variant 211) = channels-last output through an LDS tile (timing only).
 template <int R, int NL, int M = 0, bool BF16 = false, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
@@ -700,8 +701,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int k = 0; k < NP; ++k)
         issue_pair<R, BF16, (M == 3 || M == 6) ? 1 : (M == 4 ? 2 : 0)>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
+    constexpr int C = NL * (2 * R + 1);
+    // dev variant 9 (timing only): channels-last output through a per-wave
+    // LDS tile, 16-B stores of contiguous [pixel][channel] runs
+    __shared__ __attribute__((aligned(16))) float ctile[M == 9 ? 4 * 64 * C : 1];
     auto sink = [&](int ch, float v) {
-        if constexpr (M == 7) {               // dev: non-temporal output stores
+        if constexpr (M == 9) {
+            ctile[(threadIdx.x >> 6) * 64 * C + (threadIdx.x & 63) * C + ch] = v;
+        } else if constexpr (M == 7) {        // dev: non-temporal output stores
             if (q.active) __builtin_nontemporal_store(v, q.outp + (long long)ch * a.HW);
         } else {
             if (q.active && (M != 1 || v == 1234.5f)) q.outp[(long long)ch * a.HW] = v;
@@ -709,6 +716,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     };
 #pragma unroll
     for (int k = 0; k < NP; ++k) finish_pair<R, M == 2, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink);
+    if constexpr (M == 9) {
+        // the wave's tile is private and LDS runs a wave's operations in order
+        const int lane = threadIdx.x & 63;
+        const long long pw = q.pblk + (threadIdx.x & ~63);
+        const float *t = ctile + (threadIdx.x >> 6) * 64 * C;
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) {
+            const int e = (k * 64 + lane) * 4;             // element of the wave's [64][C] run
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(t + e);
+            if (pw + e / C < a.P) *reinterpret_cast<f32x4 *>(a.out + pw * C + e) = v;
+        }
+    }
 }
 
 #ifdef RAFTCORR_DEV
@@ -769,7 +788,9 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
             hipLaunchKernelGGL((lookup_pair_stamped_kernel<R>), dim3(nblk), dim3(256), 0, s, a);
             return hipGetLastError();
         }
-        if (a.levels == 4 && v >= 201 && v <= 209) {
+        if (a.levels == 4 && v >= 201 && v <= 211) {
+            if (v == 211 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 9>), dim3(nblk), dim3(256), 0, s, a);
+            if (v == 211 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 9, true>), dim3(nblk), dim3(256), 0, s, a);
             // 208 / 209: at least 5 / 6 waves per SIMD (register cap)
             if (v == 208 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 5>), dim3(nblk), dim3(256), 0, s, a);
             if (v == 208 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 5>), dim3(nblk), dim3(256), 0, s, a);
