@@ -368,6 +368,9 @@ def main():
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     ap.add_argument("--mfma", default=os.path.join(ROOT, "profiles", "mfma.json"),
                     help="PMC MFMA-busy fractions per kernel (written by tools/pmc_sq.py)")
+    ap.add_argument("--channels-last", action="store_true",
+                    help="lookup output in NHWC memory order (CorrBlock1D(channels_last=True): "
+                         "same shape and values)")
     ap.add_argument("--no-backward", action="store_true",
                     help="skip the corr-path backward timing (sceneflow only)")
     args = ap.parse_args()
@@ -408,7 +411,7 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record()
-        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last)
         if ev is not None:
             ev[1].record()
         for it in range(iters):
@@ -462,7 +465,7 @@ def main():
             be = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(5)]
             for e0, e1 in be:
                 e0.record()
-                CorrBlock1D(f1, f2, num_levels=L, radius=r)
+                CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last)
                 e1.record()
             torch.cuda.synchronize()
             build_ms = sum(e0.elapsed_time(e1) for e0, e1 in be) / len(be)
@@ -471,7 +474,7 @@ def main():
         # A device-side sleep first lets the host queue every launch before the
         # GPU reaches them, so no event pair spans a host gap; median over 3
         # passes of all launches.
-        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last)
         per_launch = []
         for _ in range(3):
             le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
@@ -566,7 +569,8 @@ def main():
                    + (f" (rows sharded over {world} ranks)" if row_shard else ""),
                    "config": args.config, "global_batch": job_pairs,
                    "fmap": [B, D, H, W1], "W2": W2, "levels": L, "radius": r, "iters": iters,
-                   "parallelism": (f"row-shard x{world}" if row_shard else f"batch-shard x{world}")},
+                   "parallelism": (f"row-shard x{world}" if row_shard else f"batch-shard x{world}"),
+                   "corr_out_layout": "channels_last" if args.channels_last else "nchw"},
         "roofline": dominant,
         "roofline_volume": roof_volume,
         "roofline_lookup": roof_lookup,

@@ -63,6 +63,13 @@ extern "C" {
 #define RC_SHADOW_OFFSET(rows, ld, esize) \
     ((((long long)(rows) * (long long)(ld) * (long long)(esize) + 127) / 128) * 128 + 64)
 
+/* Flag OR-ed into the pyr_dtype of rc_corr_lookup_chain / rc_corr_lookup_step
+ * (ABI v5): write the lookup output channels-last, out[((b*H + h)*W1 + w)*C + c]
+ * with C = levels*(2r+1) -- the (B, C, H, W1) tensor in NHWC memory order
+ * (torch.channels_last), the same values.  Pair kernel only (2 levels, or 4
+ * with level 2 given); RC_EUNSUPPORTED otherwise. */
+#define RC_OUT_CHANNELS_LAST 0x10000
+
 /* return codes */
 #define RC_OK            0
 #define RC_EINVAL        1  /* bad shape / pointer / alignment / parameter */

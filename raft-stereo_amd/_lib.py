@@ -19,6 +19,7 @@ RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
 ABI_VERSION = 5
 RC_SHADOW = 0xFF00  # pyr_dtype flags: every stored level carries a line-phase shadow copy
+RC_OUT_CHANNELS_LAST = 0x10000   # pyr_dtype flag: NHWC lookup output (pair kernel)
 
 
 def shadow_level(l):

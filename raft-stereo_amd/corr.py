@@ -296,7 +296,20 @@ def _chain_args(pyramid, num_levels, shadow=False):
     return lv, ptrs, widths, lds, _dtype_code(dt) | _shadow_flags(shadow, lv)
 
 
-def lookup_chain(pyramid, coords, num_levels, radius, shadow=False):
+def _lookup_out(B, C, H, W1, device, channels_last):
+    """(B, C, H, W1) fp32 lookup output; channels_last: NHWC memory order
+    (the C-ABI's RC_OUT_CHANNELS_LAST), same shape and values."""
+    if channels_last:
+        return torch.empty((B, H, W1, C), dtype=torch.float32, device=device).permute(0, 3, 1, 2)
+    return torch.empty((B, C, H, W1), dtype=torch.float32, device=device)
+
+
+def _pair_layout(pyramid, num_levels):
+    """The pair kernel serves this request (include/raftcorr.h, chain_kind)."""
+    return num_levels == 2 or (num_levels == 4 and len(pyramid) > 2 and pyramid[2] is not None)
+
+
+def lookup_chain(pyramid, coords, num_levels, radius, shadow=False, channels_last=False):
     """rc_corr_lookup_chain: same result as :func:`lookup` for a pyramid whose
     levels are the avg-pool chain of level 0 (what :func:`build_pyramid`
     writes).  Entries may be None: with 2 levels, or 4 levels and level 2
@@ -304,16 +317,20 @@ def lookup_chain(pyramid, coords, num_levels, radius, shadow=False):
     reads levels 0 and 1 and derives the rest (include/raftcorr.h)."""
     x, cbs = _check_coords(pyramid, coords)
     B, _, H, W1 = coords.shape
-    out = torch.empty((B, num_levels * (2 * radius + 1), H, W1), dtype=torch.float32,
-                      device=coords.device)
+    cl = channels_last and _pair_layout(pyramid, num_levels)
+    out = _lookup_out(B, num_levels * (2 * radius + 1), H, W1, coords.device, cl)
     if B * H * W1 == 0:
         return out
     keep, ptrs, widths, lds, dt = _chain_args(pyramid, num_levels, shadow)
+    if cl:
+        dt |= _lib.RC_OUT_CHANNELS_LAST
     with torch.cuda.device(coords.device):
         rc = _lib.lib().rc_corr_lookup_chain(
             ptrs, widths, lds, dt, num_levels, radius, x.data_ptr(), cbs, B, H, W1,
             out.data_ptr(), _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup_chain")
+    if channels_last and not cl:
+        out = out.contiguous(memory_format=torch.channels_last)
     return out
 
 
@@ -460,9 +477,13 @@ class CorrBlock1D:
     """model.py:283-326, on the gfx950 kernels (see module docstring)."""
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
-                 lazy_levels=None, shadow=None):
+                 lazy_levels=None, shadow=None, channels_last=False):
         self.num_levels = num_levels
         self.radius = radius
+        # lookup outputs in NHWC memory order (torch.channels_last): same
+        # shape and values; written by the pair kernel as contiguous per-wave
+        # runs instead of one 256-B piece per channel plane (DESIGN.md §3.2e)
+        self.channels_last = bool(channels_last)
         if pyramid_dtype is None:
             low = fmap1.dtype in (torch.bfloat16, torch.float16)
             pyramid_dtype = torch.bfloat16 if low else torch.float32
@@ -535,8 +556,10 @@ class CorrBlock1D:
 
     def _lookup(self, coords):
         if self._chain:
-            return lookup_chain(self._levels, coords, self.num_levels, self.radius, self._shadow)
-        return lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
+            return lookup_chain(self._levels, coords, self.num_levels, self.radius, self._shadow,
+                                self.channels_last)
+        out = lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
+        return out.contiguous(memory_format=torch.channels_last) if self.channels_last else out
 
     def __call__(self, coords):
         if self._token is not None and torch.is_grad_enabled():
@@ -575,19 +598,24 @@ class CorrBlock1D:
             raise RuntimeError("lookup_step: out must be a contiguous fp32 (B, 2, H, W1) tensor")
         flow = torch.empty_like(c1)
         L, r = self.num_levels, self.radius
-        corr = torch.empty((B, L * (2 * r + 1), H, W1), dtype=torch.float32, device=c1.device)
+        cl = self.channels_last and self._chain and _pair_layout(self._levels, L)
+        corr = _lookup_out(B, L * (2 * r + 1), H, W1, c1.device, cl)
         if B * H * W1 == 0:
             return corr, new, flow
         if self._chain:
             keep, ptrs, widths, lds, dt = _chain_args(self._levels, L, self._shadow)
         else:
             keep, ptrs, widths, lds, dt = _level_args(self.corr_pyramid, L)
+        if cl:
+            dt |= _lib.RC_OUT_CHANNELS_LAST
         with torch.cuda.device(c1.device):
             rc = _lib.lib().rc_corr_lookup_step(
                 ptrs, widths, lds, dt, L, r, int(self._chain), c1.data_ptr(),
                 d.data_ptr() if d is not None else None, new.data_ptr(), flow.data_ptr(),
                 B, H, W1, corr.data_ptr(), _stream(c1.device))
         _lib.check(rc, "rc_corr_lookup_step")
+        if self.channels_last and not cl:
+            corr = corr.contiguous(memory_format=torch.channels_last)
         return corr, new, flow
 
     def lookup_convc1(self, coords, weight, bias=None, relu=True):

@@ -280,14 +280,18 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
     int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty, true);
     if (rc) return rc;
+    const bool cl = (pyr_dtype & RC_OUT_CHANNELS_LAST) != 0;
     pyr_dtype &= 0xFF;
     bool pair;
     if ((rc = chain_kind("rc_corr_lookup_chain", pyr, widths, levels, radius, &pair))) return rc;
     if (pyr_dtype == RC_BF16 && !pair)
         return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: a bf16 pyramid needs the pair layout "
                     "(2 levels, or 4 with level 2 given)");
+    if (cl && !pair)
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: RC_OUT_CHANNELS_LAST needs the pair layout");
     if (empty) return RC_OK;
     a.out = out;
+    a.out_cl = cl;
     if ((rc = chain_strides("rc_corr_lookup_chain", a, pair, pyr_dtype == RC_BF16))) return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     return hip_rc(pair ? rc_launch_lookup_pair(a, radius, pyr_dtype == RC_BF16, s)
@@ -306,6 +310,7 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
     int rc = prep_lookup("rc_corr_lookup_step", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords1, 2L * H * W1, B, H, W1, out, a, &empty, chain != 0);
     if (rc || empty) return rc;
+    const bool cl = (pyr_dtype & RC_OUT_CHANNELS_LAST) != 0;
     pyr_dtype &= 0xFF;
     if (!coords1_out || !flow_out)
         return fail(RC_EINVAL, "rc_corr_lookup_step: null coords1_out / flow_out");
@@ -316,7 +321,10 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
             return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: a bf16 pyramid needs the pair layout");
         if ((rc = chain_strides("rc_corr_lookup_step", a, pair, pyr_dtype == RC_BF16))) return rc;
     }
+    if (cl && !pair)
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: RC_OUT_CHANNELS_LAST needs the pair layout");
     a.out = out;
+    a.out_cl = cl;
     a.step = 1;
     a.W1 = W1;
     a.delta = delta;

@@ -127,6 +127,7 @@ struct LookupArgs {
     // line-phase shadow copy of level i at (char*)lvl[i] + shadow[i] bytes
     // (0 = none); read by the pair kernel (RC_SHADOW, ABI v5)
     long long shadow[kMaxLevels];
+    int out_cl;               // channels-last output out[p*C + ch] (pair kernel; ABI v5)
 };
 
 // Backward of the lookup: level gradients (fp32, row stride ld[i] % 4 == 0).

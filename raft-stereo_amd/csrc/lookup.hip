@@ -687,8 +687,9 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
 // probes PH 1 / 2 (timing only: wrong values), 5 = hardware block order
 // (no XCD remap; same values), 6 = PH 1, 7 = non-temporal output stores;
 // the WPE parameter (dev variants 208/209) caps registers for 5/6 waves/SIMD;
-// 9 (variant 211) = channels-last output through an LDS tile (timing only).
-template <int R, int NL, int M = 0, bool BF16 = false, int WPE = 1>
+// 9 (variant 211) = the channels-last store path writing into an NCHW
+// buffer (timing A/B of the two layouts on the same output tensor).
+template <int R, int NL, int M = 0, bool BF16 = false, int WPE = 1, bool CL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
     constexpr int NP = NL / 2;                        // spans per pixel
@@ -702,11 +703,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (int k = 0; k < NP; ++k)
         issue_pair<R, BF16, (M == 3 || M == 6) ? 1 : (M == 4 ? 2 : 0)>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
     constexpr int C = NL * (2 * R + 1);
-    // dev variant 9 (timing only): channels-last output through a per-wave
-    // LDS tile, 16-B stores of contiguous [pixel][channel] runs
-    __shared__ __attribute__((aligned(16))) float ctile[M == 9 ? 4 * 64 * C : 1];
+    // CL: channels-last output (RC_OUT_CHANNELS_LAST), out[p*C + ch].  A
+    // wave's 64 pixels own one contiguous run of 64*C floats; it is gathered
+    // in a per-wave LDS tile and written as 16-B vectors, 1 KB per store
+    // instruction (instead of C dword stores, 256 B each, to C channel planes)
+    constexpr bool TILE = CL || M == 9;
+    __shared__ __attribute__((aligned(16))) float ctile[TILE ? 4 * 64 * C : 1];
     auto sink = [&](int ch, float v) {
-        if constexpr (M == 9) {
+        if constexpr (TILE) {
             ctile[(threadIdx.x >> 6) * 64 * C + (threadIdx.x & 63) * C + ch] = v;
         } else if constexpr (M == 7) {        // dev: non-temporal output stores
             if (q.active) __builtin_nontemporal_store(v, q.outp + (long long)ch * a.HW);
@@ -716,16 +720,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     };
 #pragma unroll
     for (int k = 0; k < NP; ++k) finish_pair<R, M == 2, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink);
-    if constexpr (M == 9) {
-        // the wave's tile is private and LDS runs a wave's operations in order
+    if constexpr (TILE) {
+        // the wave's tile is private and LDS runs a wave's operations in
+        // order: no barrier.  The run starts 256*C-byte aligned.
         const int lane = threadIdx.x & 63;
         const long long pw = q.pblk + (threadIdx.x & ~63);
         const float *t = ctile + (threadIdx.x >> 6) * 64 * C;
+        const long long lim = (a.P - pw < 64 ? a.P - pw : 64) * C;   // valid elements of the run
 #pragma unroll
-        for (int k = 0; k < C / 4; ++k) {
+        for (int k = 0; k < (16 * C + 63) / 64; ++k) {
             const int e = (k * 64 + lane) * 4;             // element of the wave's [64][C] run
+            if (e >= 64 * C || e >= lim) continue;
             const f32x4 v = *reinterpret_cast<const f32x4 *>(t + e);
-            if (pw + e / C < a.P) *reinterpret_cast<f32x4 *>(a.out + pw * C + e) = v;
+            if (e + 4 <= lim) {
+                *reinterpret_cast<f32x4 *>(a.out + pw * C + e) = v;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (e + j < lim) a.out[pw * C + e + j] = v[j];
+            }
         }
     }
 }
@@ -816,12 +829,23 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
         }
     }
 #endif
+    const bool cl = a.out_cl != 0;
     if (a.levels == 4) {
-        if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true>), dim3(nblk), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+        if (cl) {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+        } else {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+        }
     } else if (a.levels == 2) {
-        if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true>), dim3(nblk), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+        if (cl) {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, false, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+        } else {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+        }
     } else {
         return hipErrorInvalidValue;
     }

@@ -111,3 +111,17 @@ def test_shadow_window_validation():
     # the same request without the flag passes validation up to the launch
     # (not attempted here: H*W1 rows of fake pointers) -- only the flag differs
     assert _build(pdt=_lib.RC_F32 | _lib.RC_SHADOW, B=0) == _lib.RC_OK
+
+
+def test_channels_last_flag_needs_pair_layout():
+    """RC_OUT_CHANNELS_LAST is served by the pair kernel only: a 3-level
+    (level-1 chain) request with it is refused before any launch."""
+    L = _lib.lib()
+    text = open(_lib.HEADER).read()
+    m = re.search(r"#define RC_OUT_CHANNELS_LAST\s+(0x[0-9a-fA-F]+)", text)
+    assert m and int(m.group(1), 16) == _lib.RC_OUT_CHANNELS_LAST
+    ptrs = _lib.ptr_array([ctypes.c_void_p(0x1000), ctypes.c_void_p(0x2000), None])
+    w = _lib.int_array([64, 32, 16])
+    rc = L.rc_corr_lookup_chain(ptrs, w, None, _lib.RC_F32 | _lib.RC_OUT_CHANNELS_LAST, 3, 4,
+                                ctypes.c_void_p(0x3000), 0, 1, 2, 64, ctypes.c_void_p(0x4000), None)
+    assert rc == _lib.RC_EUNSUPPORTED and b"pair" in L.rc_last_error()
