@@ -32,9 +32,33 @@ def test_disparity_matches_reference(name):
     print(f"{name}: final MAE {mae[-1]:.2e} px, max |d| {np.abs(disp - z['disparity']).max():.2e}")
 
 
+def test_bf16_corr_path_disparity_bound():
+    """The bf16 corr path alone (fmaps rounded to bf16, bf16 MFMA volume, bf16
+    pyramid; the rest of the network fp32) against the reference's fp32
+    golden: final-disparity MAE within north_star's 0.01 px bar at every
+    iteration (SURVEY §8d probe: 4.5e-4 px after 32 iterations)."""
+    import functools
+    case = CASES["e2e_default"]
+    z = load(f"{GOLDEN}/e2e_default.npz")
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs(**case["args"]),
+                       corr_block=functools.partial(CorrBlock1D, pyramid_dtype=torch.bfloat16))
+    model = model.eval().cuda()
+    with torch.no_grad():
+        flows = model(torch.from_numpy(z["image1"]).cuda(), torch.from_numpy(z["image2"]).cuda(),
+                      iters=int(z["iters"]))
+    disp = np.stack([f[:, 0].cpu().numpy() for f in flows], 0)
+    mae = np.abs(disp - z["disparity"]).mean(axis=(1, 2, 3))
+    assert (mae <= MAE_PX).all(), f"per-iteration MAE {mae}"
+    print(f"bf16 corr path: final MAE {mae[-1]:.2e} px")
+
+
 def test_bf16_autocast_runs():
-    """Mixed precision: the reference crashes here; we accept the
-    half-precision fmaps and stay within a loose bound of the fp32 result."""
+    """Whole-network mixed precision (every conv in bf16 too, not just the
+    corr path): the reference crashes here; we accept the
+    half-precision fmaps and stay within a loose bound of the fp32 result --
+    the convolutions' bf16 rounding, not the corr path, sets this error (the
+    corr path's own bf16 bound is test_bf16_corr_path_disparity_bound)."""
     case = CASES["e2e_default"]
     z = load(f"{GOLDEN}/e2e_default.npz")
     torch.manual_seed(0)
