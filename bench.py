@@ -368,12 +368,17 @@ def main():
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     ap.add_argument("--mfma", default=os.path.join(ROOT, "profiles", "mfma.json"),
                     help="PMC MFMA-busy fractions per kernel (written by tools/pmc_sq.py)")
-    ap.add_argument("--channels-last", action="store_true",
+    ap.add_argument("--channels-last", action="store_true", default=None,
                     help="lookup output in NHWC memory order (CorrBlock1D(channels_last=True): "
-                         "same shape and values)")
+                         "same shape and values); default for the bf16 config (kitti), whose "
+                         "output does not fit the Infinity Cache (DESIGN.md §3.2f)")
+    ap.add_argument("--nchw", dest="channels_last", action="store_false",
+                    help="force the reference's NCHW-contiguous lookup output")
     ap.add_argument("--no-backward", action="store_true",
                     help="skip the corr-path backward timing (sceneflow only)")
     args = ap.parse_args()
+    if args.channels_last is None:   # NHWC output where it goes to HBM (the bf16 config)
+        args.channels_last = args.config in BF16_CONFIGS
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
