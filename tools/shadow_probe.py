@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--row-align", type=int, default=16,
                     help="row stride granule of the stored levels in bytes (corr._ROW_ALIGN_BYTES)")
     ap.add_argument("--settings", default="none,l0,l2,l0+l2")
+    ap.add_argument("--channels-last", action="store_true", help="NHWC lookup output")
     a = ap.parse_args()
     from raft_stereo_amd import corr as rcorr
     rcorr._ROW_ALIGN_BYTES = a.row_align
@@ -45,7 +46,8 @@ def main():
                 torch.cuda._sleep(2_000_000)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, shadow=sh)
+                blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, shadow=sh,
+                                  channels_last=a.channels_last)
                 e1.record()
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
                 ev[0].record()
