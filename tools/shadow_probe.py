@@ -27,7 +27,13 @@ def main():
                     help="row stride granule of the stored levels in bytes (corr._ROW_ALIGN_BYTES)")
     ap.add_argument("--settings", default="none,l0,l2,l0+l2")
     ap.add_argument("--channels-last", action="store_true", help="NHWC lookup output")
+    ap.add_argument("--dev-variant", default="",
+                    help="RAFTCORR_LOOKUP_VARIANT for the lookups (libraftcorr_dev.so)")
     a = ap.parse_args()
+    if a.dev_variant:
+        from raft_stereo_amd import _lib
+        _lib.dev_library().__enter__()
+        os.environ["RAFTCORR_LOOKUP_VARIANT"] = a.dev_variant
     from raft_stereo_amd import corr as rcorr
     rcorr._ROW_ALIGN_BYTES = a.row_align
     cfg = bench.CONFIGS[a.config]
