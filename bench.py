@@ -383,10 +383,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RAFTCORR_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several
+    # ranks sharing the GPUs there are (collectives host-side); default RCCL
+    backend = os.environ.get("RAFTCORR_BENCH_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    local_dev = local % ndev if backend != "nccl" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group(backend)
+    device = torch.device("cuda", local_dev)
     torch.cuda.set_device(device)
 
     cfg = CONFIGS[args.config]
