@@ -74,6 +74,9 @@ ROW_SHARD_CONFIGS = {"middlebury"}
 # BASELINE configs[2]: "batch 64 ... batch-sharded across 2/4/8 GPUs" -- the
 # config's B is the GLOBAL batch, split over the ranks (strong scaling)
 GLOBAL_BATCH_CONFIGS = {"kitti"}
+# small latency-bound config: every level stored, one wave per level per
+# 64 pixels in the lookup (CorrBlock1D(low_latency=True))
+LOW_LATENCY_CONFIGS = {"realtime"}
 
 
 def make_inputs(cfg, device, seed, dtype=torch.float32):
@@ -424,7 +427,8 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record()
-        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last)
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
+                          low_latency=args.config in LOW_LATENCY_CONFIGS)
         if ev is not None:
             ev[1].record()
         for it in range(iters):
@@ -478,7 +482,8 @@ def main():
             be = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(5)]
             for e0, e1 in be:
                 e0.record()
-                CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last)
+                CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
+                          low_latency=args.config in LOW_LATENCY_CONFIGS)
                 e1.record()
             torch.cuda.synchronize()
             build_ms = sum(e0.elapsed_time(e1) for e0, e1 in be) / len(be)
@@ -487,7 +492,8 @@ def main():
         # A device-side sleep first lets the host queue every launch before the
         # GPU reaches them, so no event pair spans a host gap; median over 3
         # passes of all launches.
-        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last)
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
+                          low_latency=args.config in LOW_LATENCY_CONFIGS)
         per_launch = []
         for _ in range(3):
             le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
@@ -546,6 +552,7 @@ def main():
     pair = blk._chain and (L == 2 or (L == 4 and 2 in written))
     lname = (f"rc::lookup_pair_kernel<{r},{L}>" if pair else
              f"rc::lookup_chain_kernel<{r},{L},0>" if blk._chain
+             else f"rc::lookup_levelpar_kernel<{r},{'true' if bf16 else 'false'}>" if P < 65536 and L <= 4
              else f"rc::lookup_kernel<{r},0,{'true' if bf16 else 'false'},true>")
     ltraffic = traffic.get("lookup_pair_bytes" if pair else
                            "lookup_chain_bytes" if blk._chain else "lookup_bytes")

@@ -477,7 +477,7 @@ class CorrBlock1D:
     """model.py:283-326, on the gfx950 kernels (see module docstring)."""
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
-                 lazy_levels=None, shadow=None, channels_last=False):
+                 lazy_levels=None, shadow=None, channels_last=False, low_latency=False):
         self.num_levels = num_levels
         self.radius = radius
         # lookup outputs in NHWC memory order (torch.channels_last): same
@@ -505,6 +505,12 @@ class CorrBlock1D:
         self._chain = (1 <= radius <= 4 and fmap2.shape[-1] <= 65536 and
                        (num_levels in (2, 3, 4) if pyramid_dtype == torch.float32 else
                         num_levels in (2, 4) if pyramid_dtype == torch.bfloat16 else False))
+        # low_latency (small inputs, e.g. the realtime config): store every
+        # level and use the per-level lookup, whose launcher gives each level
+        # its own wave below 64K pixels (lookup_levelpar_kernel, DESIGN.md
+        # §3.2g): a shorter dependent chain per launch, bit-identical values
+        if low_latency:
+            self._chain = False
         lazy = self._chain if lazy_levels is None else (bool(lazy_levels) and self._chain)
         with torch.no_grad():
             if lazy and num_levels == 3:

@@ -225,6 +225,36 @@ void lookup_kernel(LookupArgs a) {
     }
 }
 
+// Small problems (the realtime config: 19,200 pixels): a launch then lasts
+// about one wave's chain of window loads and tap math, so a block gives each
+// LEVEL its own wave -- wave i of block b looks up level i for pixels
+// [64b, 64b+64) -- which shortens that chain ~L-fold.  Per level the code is
+// lookup_kernel's (issue_level / finish_level): bit-identical results.  In
+// the fused loop step every wave reads the pixel's coords before the block
+// barrier and only wave 0 writes the advanced coords and flow after it (the
+// outputs may alias coords1).
+template <int R, bool BF16>
+__global__ __launch_bounds__(256) void lookup_levelpar_kernel(LookupArgs a) {
+    constexpr int T = 2 * R + 1;
+    const int i = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // this wave's level
+    const long long pblk = (long long)blockIdx.x * 64;
+    const long long p = pblk + (threadIdx.x & 63);
+    const bool active = p < a.P;
+    const long long pp = active ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    const float x = pixel_x(a, bimg, rem, false);
+    if (a.step) {                                       // block-uniform
+        __syncthreads();
+        if (i == 0) (void)pixel_x(a, bimg, rem, active);
+    }
+    float *outp = a.out + bimg * (long long)(a.levels * T) * a.HW + rem;
+    LevelWindow<R, BF16> lw;
+    issue_level<R, BF16, true>(lw, a, i, x, pblk, pp - pblk);
+    finish_level<R, BF16>(lw, a, i, pblk, pp - pblk, [&](int t, float v) {
+        if (active) outp[(long long)(i * T + t) * a.HW] = v;
+    });
+}
+
 // ---- lookup over a pool-chain pyramid: levels >= 2 derived from level 1 ----
 // When the levels are the avg_pool chain of level 0 -- the pyramid
 // rc_corr_build writes -- element j of level i >= 2 is the pairwise-mean tree
@@ -963,6 +993,9 @@ static void launch_k(const LookupArgs &a, hipStream_t s) {
 // runtime-loop kernel (one dependent memory round trip per level): use
 // 64-thread blocks and issue every level's loads up front instead.
 constexpr long long kSmallP = 256LL * 256 * 2;
+// Below this many pixels one wave per (64 pixels, level) still leaves the
+// chip under-filled or about full: lookup_levelpar_kernel.
+constexpr long long kLevelParP = 64LL * 1024;
 
 template <int R>
 static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream_t s) {
@@ -973,7 +1006,11 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
 #ifndef RAFTCORR_DEV
     variant = 0;
 #endif
-    if (variant == 0 && a.P < kSmallP && unroll) {
+    if (variant == 0 && a.P < kLevelParP && a.levels <= 4) {
+        const unsigned nblk = (unsigned)((a.P + 63) / 64);
+        if (bf16) hipLaunchKernelGGL((lookup_levelpar_kernel<R, true>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
+        else hipLaunchKernelGGL((lookup_levelpar_kernel<R, false>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
+    } else if (variant == 0 && a.P < kSmallP && unroll) {
         if (a.levels == 4) {
             if (bf16) launch_k<R, 4, true, true, 64>(a, s);
             else launch_k<R, 4, false, true, 64>(a, s);
