@@ -186,7 +186,14 @@ int rc_corr_lookup_step(const void *const *pyr, const int *widths, const long *p
  *          radius <= 4, the gradients of levels 1 and 3 are added, already
  *          through avg_pool2d's backward (/2 to both children), to levels 0
  *          and 2; pass such buffers to rc_corr_build_backward with levels = 3
- *          and grad_pyr[1] = NULL. */
+ *          and grad_pyr[1] = NULL.
+ *   levels | RC_SHADOW_LEVEL(0) / RC_SHADOW_LEVEL(2) (4-level pair layout
+ *          only, else RC_EUNSUPPORTED): the allocation of grad_pyr[l] also
+ *          holds a zeroed copy at RC_SHADOW_OFFSET(B*H*W1, grad_ld[l], 4)
+ *          bytes; each pixel's span goes to the copy in which it touches
+ *          fewer 128-B lines.  Pass the same bits to rc_corr_build_backward,
+ *          which sums the copies.  Measured not to pay at config 2
+ *          (DESIGN.md §3.4b); off by default. */
 int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long *grad_ld,
                             int levels, int radius, const float *coords_x,
                             long coord_batch_stride, int B, int H, int W1,
@@ -201,7 +208,8 @@ int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long
  *   B*H*W1 rows of W2 >> l, row stride grad_ld[l] (grad_ld[0] % 4 == 0).
  *   fmap_dtype RC_F32 only.  When B*H*W1 == 0 nothing is written.
  *   levels == 3 with grad_pyr[1] == NULL: pair-folded gradients from
- *   rc_corr_lookup_backward's pair layout, Dl_0[k] = g_0[k] + g_2[k>>2] / 4. */
+ *   rc_corr_lookup_backward's pair layout, Dl_0[k] = g_0[k] + g_2[k>>2] / 4;
+ *   with levels | RC_SHADOW_LEVEL(0) / (2) each g_l is primary + shadow copy. */
 int rc_corr_build_backward(const void *fmap1, const void *fmap2, int fmap_dtype,
                            int B, int D, int H, int W1, int W2,
                            const void *const *grad_pyr, const long *grad_ld, int levels,

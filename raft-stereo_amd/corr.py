@@ -336,19 +336,41 @@ def lookup_chain(pyramid, coords, num_levels, radius, shadow=False, channels_las
 
 # ----------------------------------------------------------------- backward
 
-def grad_buffers(P, widths, device, pair=False):
+class _GradLevels(list):
+    """The level-gradient list, with the levels that carry an RC_SHADOW copy."""
+    shadow = frozenset()
+
+
+def grad_buffers(P, widths, device, pair=False, shadow=()):
     """Zeroed fp32 level-gradient buffers (P, W_l) with rows padded to 16 bytes
     (the padding stays zero: rc_corr_lookup_backward never touches it).
     ``pair``: the pair layout -- levels 1 and 3 are None, their gradients are
-    folded into levels 0 and 2 by the pair backward kernel."""
-    bufs = []
+    folded into levels 0 and 2 by the pair backward kernel.  ``shadow``:
+    levels (0 and/or 2 of the 4-level pair layout) whose allocation also holds
+    a zeroed RC_SHADOW copy at ``_lib.shadow_offset``; the lookup backward adds
+    each span into the copy where it touches fewer 128-B lines and the build
+    backward sums the two."""
+    shadow = frozenset(shadow)
+    if shadow and not (pair and len(widths) == 4 and shadow <= {0, 2}):
+        raise ValueError("gradient shadow copies: levels 0 and 2 of the 4-level pair layout")
+    bufs = _GradLevels()
     for l, W in enumerate(widths):
         if pair and l % 2 == 1:
             bufs.append(None)
             continue
         ld = -(-W // 4) * 4
-        bufs.append(torch.zeros((P, ld), dtype=torch.float32, device=device)[:, :W])
+        if l in shadow:
+            total = _lib.shadow_offset(P, ld, 4) + P * ld * 4
+            buf = torch.zeros(total // 4, dtype=torch.float32, device=device)[:P * ld].view(P, ld)
+        else:
+            buf = torch.zeros((P, ld), dtype=torch.float32, device=device)
+        bufs.append(buf[:, :W])
+    bufs.shadow = shadow
     return bufs
+
+
+def _grad_shadow_flags(grads):
+    return sum(_lib.shadow_level(l) for l in getattr(grads, "shadow", ()))
 
 
 def _pair_grads_ok(num_levels, radius, W0):
@@ -373,7 +395,7 @@ def lookup_backward(grads, coords, grad_out, num_levels, radius):
             _lib.ptr_array([None if t is None else t.data_ptr() for t in g]),
             _lib.int_array([W0 >> i for i in range(num_levels)]),
             _lib.long_array([W0 >> i if t is None else t.stride(0) for i, t in enumerate(g)]),
-            num_levels, radius, x.data_ptr(), cbs, B, H, W1, go.data_ptr(),
+            num_levels | _grad_shadow_flags(grads), radius, x.data_ptr(), cbs, B, H, W1, go.data_ptr(),
             _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup_backward")
 
@@ -390,6 +412,7 @@ def build_backward(fmap1, fmap2, grads):
         return torch.zeros_like(f1), torch.zeros_like(f2)
     df1, df2 = torch.empty_like(f1), torch.empty_like(f2)
     # pair layout [g0, None, g2, None] -> levels 0-2 with level 1 NULL; [g0, None] -> level 0
+    flags = _grad_shadow_flags(grads)
     if len(grads) > 1 and grads[1] is None:
         grads = [grads[0], None, grads[2]] if len(grads) > 2 else [grads[0]]
     with torch.cuda.device(f1.device):
@@ -397,7 +420,7 @@ def build_backward(fmap1, fmap2, grads):
             f1.data_ptr(), f2.data_ptr(), _lib.RC_F32, B, D, H, W1, W2,
             _lib.ptr_array([None if g is None else g.data_ptr() for g in grads]),
             _lib.long_array([W2 >> l if g is None else g.stride(0) for l, g in enumerate(grads)]),
-            len(grads), df1.data_ptr(), df2.data_ptr(), _stream(f1.device))
+            len(grads) | flags, df1.data_ptr(), df2.data_ptr(), _stream(f1.device))
     _lib.check(rc, "rc_corr_build_backward")
     return df1, df2
 
@@ -417,20 +440,29 @@ def default_shadow_levels(P, W2, num_levels, pyramid_dtype):
     return tuple(l for l in lv if shadow_fits(P, W2 >> l, pyramid_dtype))
 
 
+def default_grad_shadow_levels(P, widths, num_levels, pair):
+    """Gradient levels that get an RC_SHADOW copy by default."""
+    return ()
+
+
 class _GradState:
     """Level gradients shared by one CorrBlock1D's lookup nodes and its build
     node.  Holds no pyramid and no graph node, so no reference cycle keeps the
     pyramid alive."""
 
-    def __init__(self, P, widths, device, num_levels, radius):
+    def __init__(self, P, widths, device, num_levels, radius, grad_shadow=None):
         self.P, self.widths, self.device = P, widths, device
         self.num_levels, self.radius = num_levels, radius
         self.pair = _pair_grads_ok(num_levels, radius, widths[0])
+        if grad_shadow is None:
+            grad_shadow = default_grad_shadow_levels(P, widths, num_levels, self.pair)
+        self.grad_shadow = frozenset(grad_shadow) if self.pair and num_levels == 4 else frozenset()
         self.grads = None
 
     def accumulate(self, coords, grad_out):
         if self.grads is None:
-            self.grads = grad_buffers(self.P, self.widths, self.device, pair=self.pair)
+            self.grads = grad_buffers(self.P, self.widths, self.device, pair=self.pair,
+                                      shadow=self.grad_shadow)
         lookup_backward(self.grads, coords, grad_out, self.num_levels, self.radius)
 
     def take(self):
@@ -477,7 +509,8 @@ class CorrBlock1D:
     """model.py:283-326, on the gfx950 kernels (see module docstring)."""
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
-                 lazy_levels=None, shadow=None, channels_last=False, low_latency=False):
+                 lazy_levels=None, shadow=None, channels_last=False, low_latency=False,
+                 grad_shadow=None):
         self.num_levels = num_levels
         self.radius = radius
         # lookup outputs in NHWC memory order (torch.channels_last): same
@@ -509,6 +542,8 @@ class CorrBlock1D:
         # level and use the per-level lookup, whose launcher gives each level
         # its own wave below 64K pixels (lookup_levelpar_kernel, DESIGN.md
         # §3.2g): a shorter dependent chain per launch, bit-identical values
+        # grad_shadow: levels (0, 2 of the 4-level pair layout) whose gradient
+        # buffers get an RC_SHADOW copy; None = the default
         if low_latency:
             self._chain = False
         lazy = self._chain if lazy_levels is None else (bool(lazy_levels) and self._chain)
@@ -534,7 +569,7 @@ class CorrBlock1D:
         self._state = self._token = None
         if grad:
             self._state = _GradState(B * H * W1, [W2 >> i for i in range(num_levels)],
-                                     fmap1.device, num_levels, radius)
+                                     fmap1.device, num_levels, radius, grad_shadow)
             self._token = _BuildFn.apply(fmap1, fmap2, self._state)
 
     @property

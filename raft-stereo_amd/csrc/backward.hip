@@ -298,6 +298,7 @@ struct PairGradSpan {
     float gv[2][2 * R + 1];        // output gradients of the even / odd level
     float m, n;
     int sh, lo_e, hi_e;            // chunk shift; touched element range
+    uint32_t ph;                   // bytes to the copy this span goes to (0 or a.shadow[lo])
     bool inwin, valid;
 };
 
@@ -340,12 +341,22 @@ __device__ __forceinline__ void issue_pair_grad(PairGradSpan<R> &ps, const Looku
     const int sa = 2 * ((int)ps.m - R - 1), ea = sa & ~3;
     ps.sh = sa - ea;
     const long long ld = a.ld[lo];
-    const auto rs = make_rsrc(a.g[lo] + pblk * ld, clamp_bytes((a.P - pblk) * ld * 4));
+    // RC_SHADOW gradient copy: the span's chunks go to the
+    // copy, half a 128-B line away, in which they touch fewer lines; the
+    // build backward sums the two copies.  pblk * ld * 4 is a multiple of
+    // 4 KB, so the line phase relative to the block base is the absolute one.
+    const long long shb = a.shadow[lo];
+    ps.ph = 0;
+    if (shb && ps.hi_e >= ps.lo_e) {
+        const long long b0 = (lrow * ld + (ps.lo_e & ~3)) * 4, b1 = (lrow * ld + (ps.hi_e | 3)) * 4 + 3;
+        if (((b1 + shb) >> 7) - ((b0 + shb) >> 7) < (b1 >> 7) - (b0 >> 7)) ps.ph = (uint32_t)shb;
+    }
+    const auto rs = make_rsrc(a.g[lo] + pblk * ld, clamp_bytes((a.P - pblk) * ld * 4 + shb));
 #pragma unroll
     for (int k = 0; k < PS::NC; ++k) {
         const int cs = ea + 4 * k;
         const bool ok = cs <= ps.hi_e && cs + 3 >= ps.lo_e;   // inside the row (lo_e >= 0, hi_e < W)
-        ps.q[k] = ld4(rs, ok ? (uint32_t)((lrow * ld + cs) * 4) : 0xFFFFFF00u);
+        ps.q[k] = ld4(rs, ok ? (uint32_t)((lrow * ld + cs) * 4) + ps.ph : 0xFFFFFF00u);
     }
 }
 
@@ -431,6 +442,7 @@ __device__ __forceinline__ void finish_pair_grad(PairGradSpan<R> &ps, const Look
     // read-modify-write the touched chunks: chunk k = elements ea+4k.., span
     // index 4k+c-sh (sh in {0, 2})
     const int ea = 2 * ((int)ps.m - R - 1) - ps.sh;
+    float *wrow = reinterpret_cast<float *>(reinterpret_cast<char *>(row) + ps.ph);
 #pragma unroll
     for (int k = 0; k < PS::NC; ++k) {
         const int cs = ea + 4 * k;
@@ -443,7 +455,7 @@ __device__ __forceinline__ void finish_pair_grad(PairGradSpan<R> &ps, const Look
             const float a2 = (j2 >= 0 && j2 < NS) ? acc[j2] : 0.0f;
             w[c] += ps.sh ? a2 : a0;
         }
-        *reinterpret_cast<f32x4 *>(row + cs) = w;
+        *reinterpret_cast<f32x4 *>(wrow + cs) = w;
     }
 }
 
@@ -506,8 +518,13 @@ __device__ __forceinline__ void fold_load(const BuildBwdArgs &a, long long prow,
     // rows of level 0 are padded to a multiple of 4, so the quad is in the row
     r.g0 = *reinterpret_cast<const f32x4 *>(a.g[0] + prow * a.ld[0] + w2);
     if constexpr (NLEV == kPairFold) {      // one level-2 value per quad
+        // RC_SHADOW gradient copies: G sums the two copies of each level
+        if (a.shadow[0]) r.g0 += *reinterpret_cast<const f32x4 *>(a.g[0] + a.shadow[0] + prow * a.ld[0] + w2);
         const int k = w2 >> 2;
-        if (k < a.Wl[2]) r.lc[0] = a.g[2][prow * a.ld[2] + k];
+        if (k < a.Wl[2]) {
+            const float *g2 = a.g[2] + prow * a.ld[2] + k;
+            r.lc[0] = a.shadow[2] ? g2[0] + g2[a.shadow[2]] : g2[0];
+        }
         return;
     }
     if (NLEV >= 2 || (NLEV == 0 && a.nlev > 1)) {

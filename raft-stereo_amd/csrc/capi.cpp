@@ -342,6 +342,9 @@ extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
                                        const float *coords_x, long coord_batch_stride, int B,
                                        int H, int W1, const float *grad_out, void *stream) {
     g_err[0] = 0;
+    // RC_SHADOW_LEVEL(l) bits above the level count: gradient copies (pair layout)
+    const unsigned shmask = ((unsigned)levels >> 8) & 0xFFu;
+    levels &= 0xFF;
     rc::LookupArgs la;
     bool empty;
     int rc = prep_lookup("rc_corr_lookup_backward", grad_pyr, widths, grad_ld, RC_F32, levels,
@@ -357,6 +360,11 @@ extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
         if (!ok)
             return fail(RC_EINVAL, "rc_corr_lookup_backward: NULL gradient levels need the pair "
                         "layout (levels 2 or 4, level 1 [and 3] NULL, radius <= 4, halving widths)");
+        if (shmask && (levels != 4 || (shmask & ~0x5u)))
+            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_backward: RC_SHADOW gradient copies are "
+                        "levels 0 and 2 of the 4-level pair layout");
+    } else if (shmask) {
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_backward: RC_SHADOW needs the pair layout");
     } else {
         for (int i = 1; i < levels; ++i)
             if (!grad_pyr[i])
@@ -376,6 +384,12 @@ extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
         a.g[i] = static_cast<float *>(const_cast<void *>(la.lvl[i]));
         a.W[i] = la.W[i];
         a.ld[i] = la.ld[i];
+        if (shmask >> i & 1u) {
+            a.shadow[i] = shadow_offset(la.P, la.ld[i], 4);
+            if (a.shadow[i] + la.P * la.ld[i] * 4 > 0xFFFFFF00LL)
+                return fail(RC_EUNSUPPORTED, "rc_corr_lookup_backward: level %d with its shadow copy "
+                            "exceeds 4 GiB", i);
+        }
     }
     a.coords = coords_x;
     a.cbs = coord_batch_stride;
@@ -392,6 +406,8 @@ extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int 
                                       const long *grad_ld, int levels, float *grad_fmap1,
                                       float *grad_fmap2, void *stream) {
     g_err[0] = 0;
+    const unsigned shmask = ((unsigned)levels >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits (pair layout)
+    levels &= 0xFF;
     if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
         return fail(RC_EINVAL, "rc_corr_build_backward: bad shape B=%d D=%d H=%d W1=%d W2=%d", B, D,
                     H, W1, W2);
@@ -408,6 +424,9 @@ extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int 
     rc::BuildBwdArgs a{};
     // levels == 3 with grad_pyr[1] NULL: pair-folded gradients (levels 0, 2)
     const bool pair = levels == 3 && !grad_pyr[1];
+    if (shmask && (!pair || (shmask & ~0x5u)))
+        return fail(RC_EUNSUPPORTED, "rc_corr_build_backward: RC_SHADOW copies are levels 0 and 2 of "
+                    "the pair layout");
     for (int l = 0; l < levels; ++l) {
         const long ld = grad_ld ? grad_ld[l] : (long)(W2 >> l);
         if (pair && l == 1) {
@@ -425,6 +444,7 @@ extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int 
         a.g[l] = static_cast<const float *>(grad_pyr[l]);
         a.ld[l] = ld;
         a.Wl[l] = W2 >> l;
+        if (shmask >> l & 1u) a.shadow[l] = shadow_offset((long long)B * H * W1, ld, 4) / 4;
     }
     if (a.ld[0] % 4 != 0)
         return fail(RC_EINVAL, "rc_corr_build_backward: level-0 row stride %lld is not a multiple "

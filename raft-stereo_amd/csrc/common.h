@@ -141,6 +141,7 @@ struct LookupBwdArgs {
     long long P;
     int HW;
     int levels;
+    long long shadow[kMaxLevels];   // bytes from g[l] to its RC_SHADOW copy (pair layout), 0 = none
 };
 
 // Backward of the build: level gradients -> feature-map gradients (fp32).
@@ -155,6 +156,7 @@ struct BuildBwdArgs {
     int tm, tn1, tn2;         // 128-row d tiles; 128-col tiles over W1 (dF1) / W2 (dF2)
     float scale, sq;
     int pow2;
+    long long shadow[kMaxLevels];   // floats from g[l] to its RC_SHADOW copy (kPairFold), 0 = none
 };
 
 }  // namespace rc

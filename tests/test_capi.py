@@ -125,3 +125,28 @@ def test_channels_last_flag_needs_pair_layout():
     rc = L.rc_corr_lookup_chain(ptrs, w, None, _lib.RC_F32 | _lib.RC_OUT_CHANNELS_LAST, 3, 4,
                                 ctypes.c_void_p(0x3000), 0, 1, 2, 64, ctypes.c_void_p(0x4000), None)
     assert rc == _lib.RC_EUNSUPPORTED and b"pair" in L.rc_last_error()
+
+
+def test_grad_shadow_flag_validation():
+    """RC_SHADOW_LEVEL bits on the backward entry points:
+    levels 0 and 2 of the 4-level pair layout only, refused before any launch."""
+    L = _lib.lib()
+    f = lambda a: ctypes.c_void_p(a)  # noqa: E731
+    w = _lib.int_array([64, 32, 16, 8])
+    pair = _lib.ptr_array([f(0x1000), None, f(0x2000), None])
+    full = _lib.ptr_array([f(0x1000), f(0x2000), f(0x3000), f(0x5000)])
+    args = lambda ptrs, lv: (ptrs, w, None, lv, 4, f(0x7000), 0, 1, 2, 64, f(0x8000), None)  # noqa: E731
+    for ptrs, lv in ((full, 4 | _lib.shadow_level(0)), (pair, 4 | _lib.shadow_level(1)),
+                     (_lib.ptr_array([f(0x1000), None]), 2 | _lib.shadow_level(0))):
+        assert L.rc_corr_lookup_backward(*args(ptrs, lv)) == _lib.RC_EUNSUPPORTED
+        assert b"RC_SHADOW" in L.rc_last_error()
+    bb = lambda ptrs, lv: L.rc_corr_build_backward(  # noqa: E731
+        f(0x1000), f(0x2000), _lib.RC_F32, 1, 32, 2, 64, 64, ptrs, None, lv, f(0x3000), f(0x4000), None)
+    assert bb(full, 4 | _lib.shadow_level(0)) == _lib.RC_EUNSUPPORTED
+    assert bb(_lib.ptr_array([f(0x1000), None, f(0x2000)]), 3 | _lib.shadow_level(1)) == _lib.RC_EUNSUPPORTED
+    assert b"RC_SHADOW" in L.rc_last_error()
+    from raft_stereo_amd import corr as rcorr
+    with pytest.raises(ValueError):
+        rcorr.grad_buffers(16, [64, 32], "cpu", pair=True, shadow=(0,))
+    with pytest.raises(ValueError):
+        rcorr.grad_buffers(16, [64, 32, 16, 8], "cpu", pair=True, shadow=(1,))
