@@ -460,8 +460,10 @@ __device__ __forceinline__ void finish_pair_grad(PairGradSpan<R> &ps, const Look
 }
 
 // NL = 2 (levels 0-1) or 4 (levels 0-3); a.g[1] (and a.g[3]) are not used.
-template <int R, int NL>
-__global__ __launch_bounds__(256) void lookup_bwd_pair_kernel(LookupBwdArgs a) {
+// WPE / SEQ: dev A/B only (an occupancy floor; each pair's loads issued after
+// the previous pair's stores instead of all up front).
+template <int R, int NL, int WPE = 1, bool SEQ = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_bwd_pair_kernel(LookupBwdArgs a) {
     static_assert(NL == 2 || NL == 4, "pair backward: 2 or 4 levels");
     constexpr int NP = NL / 2, T = 2 * R + 1;
     const long long pblk = (long long)blockIdx.x * 256;
@@ -470,6 +472,15 @@ __global__ __launch_bounds__(256) void lookup_bwd_pair_kernel(LookupBwdArgs a) {
     const long long bimg = p / a.HW, rem = p - bimg * a.HW;
     const float x = a.coords[bimg * a.cbs + rem];
     const float *go = a.grad_out + bimg * (long long)(NL * T) * a.HW + rem;
+    if constexpr (SEQ) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            PairGradSpan<R> sp;
+            issue_pair_grad<R>(sp, a, 2 * k, x, go, pblk, p - pblk);
+            finish_pair_grad<R>(sp, a, 2 * k, x, p);
+        }
+        return;
+    }
     PairGradSpan<R> sp[NP];
 #pragma unroll
     for (int k = 0; k < NP; ++k) issue_pair_grad<R>(sp[k], a, 2 * k, x, go, pblk, p - pblk);
@@ -717,6 +728,18 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
     if (a.P <= 0) return hipSuccess;
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
     if (a.levels >= 2 && a.g[1] == nullptr) {   // pair-folded gradient buffers (levels 0, 2)
+#ifdef RAFTCORR_DEV
+        // dev A/B: 21/22 occupancy floors 3/4 waves per SIMD, 23 pairs in
+        // sequence, 24 both (sequence + 4 waves)
+        const int pv = rc::dev_knob("RAFTCORR_LOOKUP_BWD_VARIANT");
+        if (pv >= 21 && pv <= 24 && radius == 4 && a.levels == 4) {
+            if (pv == 21) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
+            if (pv == 22) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 4>), dim3(nblk), dim3(256), 0, s, a);
+            if (pv == 23) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+            if (pv == 24) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 4, true>), dim3(nblk), dim3(256), 0, s, a);
+            return hipGetLastError();
+        }
+#endif
 #define RC_LBWDP(RR)                                                                                 \
     if (a.levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<RR, 4>), dim3(nblk), dim3(256), 0, s, a); \
     else hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<RR, 2>), dim3(nblk), dim3(256), 0, s, a);
