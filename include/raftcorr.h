@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 5
+#define RC_ABI_VERSION 6
 
 /* element types */
 #define RC_F32  0
@@ -70,6 +70,17 @@ extern "C" {
  * with level 2 given); RC_EUNSUPPORTED otherwise. */
 #define RC_OUT_CHANNELS_LAST 0x10000
 
+/* Flag OR-ed into the pyr_dtype of rc_corr_build (ABI v6): run the exact fp32
+ * MFMA kernel (v_mfma_f32_16x16x4_f32) for fp32 fmaps and an fp32 pyramid.
+ * Without it such a build runs the split-bf16 kernel: every fp32 operand is
+ * the exact sum of three bf16 pieces and each product the sum of the six
+ * leading piece products on v_mfma_f32_16x16x32_bf16 with fp32 accumulation
+ * -- fp32 accuracy (measured at or below the fp32 MFMA chain's error against
+ * an fp64 volume) at a third of the MFMA time.  Non-finite fmap values are
+ * the exception: an inf operand gives NaN in its row's volume where the fp32
+ * GEMM gives +-inf; pass this flag for such inputs.  Ignored by bf16 builds. */
+#define RC_BUILD_EXACT_F32 0x20000
+
 /* return codes */
 #define RC_OK            0
 #define RC_EINVAL        1  /* bad shape / pointer / alignment / parameter */
@@ -95,8 +106,9 @@ const char *rc_last_error(void);
  *          don't-care values and never read).
  *   Requires (W2 >> (nbuf-1)) >= 1 (the reference raises otherwise) and
  *   16-byte aligned pointers.
- *   Arithmetic: fmap_dtype == pyr_dtype == RC_F32 runs the exact fp32 MFMA
- *   kernel (v_mfma_f32_16x16x4_f32).  Any bf16 operand (bf16 fmaps, or a
+ *   Arithmetic: fmap_dtype == pyr_dtype == RC_F32 runs the split-bf16 fp32
+ *   kernel (ABI v6; see RC_BUILD_EXACT_F32, which selects the exact fp32 MFMA
+ *   kernel v_mfma_f32_16x16x4_f32 instead).  Any bf16 operand (bf16 fmaps, or a
  *   bf16 pyramid requested for fp32 fmaps, which are rounded to bf16 on
  *   load) runs the bf16 MFMA kernel (v_mfma_f32_16x16x32_bf16, fp32
  *   accumulation); pooling is done on the fp32 accumulators either way. */

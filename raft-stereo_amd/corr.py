@@ -39,6 +39,8 @@ Appendix A D9; their gradients are computed in fp32): they, or
 an explicit ``pyramid_dtype=torch.bfloat16``, select the bf16 MFMA kernel and
 a bf16 pyramid (bf16-level tolerance).
 """
+import warnings
+
 import torch
 
 from . import _lib
@@ -148,12 +150,16 @@ def _row_stride(t):
     return t.stride(0) if t.shape[0] > 1 else t.shape[-1]
 
 
-def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, skip=(), shadow=False):
+def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, skip=(), shadow=False,
+                  exact_f32=False):
     """Run rc_corr_build: returns ``nbuf`` tensors (B*H*W1, 1, 1, W2 >> l)
     (row-padded views when ``pad``; values identical either way).  Levels in
     ``skip`` (>= 1) are computed by the fused epilogue but not stored: their
     entries are None.  ``shadow``: every stored level also gets its RC_SHADOW
-    copy (same values, half a 128-B line later; read by the pair lookup)."""
+    copy (same values, half a 128-B line later; read by the pair lookup).
+    ``exact_f32``: fp32 fmaps and pyramid run the exact fp32 MFMA kernel
+    (RC_BUILD_EXACT_F32) instead of the split-bf16 one (fp32 accuracy,
+    DESIGN.md §3.1c)."""
     B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
     if (W2 >> (nbuf - 1)) < 1:
         raise RuntimeError(
@@ -175,7 +181,8 @@ def build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype=torch.float32, pad=True, ski
             f1.data_ptr(), f2.data_ptr(), _dtype_code(f1.dtype), B, D, H, W1, W2,
             _lib.ptr_array([None if t is None else t.data_ptr() for t in pyr]),
             _lib.long_array([W2 >> l if t is None else _row_stride(t) for l, t in enumerate(pyr)]),
-            nbuf, _dtype_code(pyramid_dtype) | _shadow_flags(shadow, pyr), _stream(f1.device))
+            nbuf, _dtype_code(pyramid_dtype) | _shadow_flags(shadow, pyr) |
+            (_lib.RC_BUILD_EXACT_F32 if exact_f32 else 0), _stream(f1.device))
     _lib.check(rc, "rc_corr_build")
     return pyr
 
@@ -445,6 +452,19 @@ def default_grad_shadow_levels(P, widths, num_levels, pair):
     return ()
 
 
+def _check_grad_shadow(grad_shadow, num_levels, radius, W0):
+    """Validate a ``grad_shadow`` request at construction: levels
+    0 and 2 only, and only with the 4-level pair gradient layout."""
+    req = frozenset(int(l) for l in grad_shadow)
+    if not req:
+        return
+    if not req <= {0, 2}:
+        raise ValueError(f"grad_shadow={sorted(req)}: gradient shadow copies are levels 0 and 2")
+    if not (num_levels == 4 and _pair_grads_ok(num_levels, radius, W0)):
+        raise ValueError("grad_shadow needs the 4-level pair gradient layout (num_levels=4, "
+                         f"radius <= 4, W2 <= 65536); got num_levels={num_levels}, radius={radius}")
+
+
 class _GradState:
     """Level gradients shared by one CorrBlock1D's lookup nodes and its build
     node.  Holds no pyramid and no graph node, so no reference cycle keeps the
@@ -510,7 +530,7 @@ class CorrBlock1D:
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
                  lazy_levels=None, shadow=None, channels_last=False, low_latency=False,
-                 grad_shadow=None):
+                 grad_shadow=None, exact_f32=False):
         self.num_levels = num_levels
         self.radius = radius
         # lookup outputs in NHWC memory order (torch.channels_last): same
@@ -527,6 +547,8 @@ class CorrBlock1D:
             raise RuntimeError(
                 f"CorrBlock1D: W2={W2} is too narrow for {num_levels} pooling steps: "
                 "avg_pool2d output size is too small (model.py:294)")
+        if grad_shadow is not None:      # refused before the build is paid for
+            _check_grad_shadow(grad_shadow, num_levels, radius, W2)
         # fp32 pyramids with 2-4 levels use a pool-chain lookup that reads two
         # stored levels and recomputes the others bit for bit (DESIGN.md §3.2c,
         # §3.2d): 2 or 4 levels -> levels 0 and 2 stored (the pair kernel), 3
@@ -563,8 +585,19 @@ class CorrBlock1D:
                 shadow = default_shadow_levels(B * H * W1, W2, num_levels, pyramid_dtype)
             self._shadow = (frozenset(l for l in _shadow_levels(shadow, nbuf) if l not in skip)
                             if pair else frozenset())
+            # an explicit request is held to the same 4 GiB window as the
+            # default: a copy the pair kernel cannot address would cost its
+            # build writes and make every lookup fail
+            too_big = sorted(l for l in self._shadow
+                             if not shadow_fits(B * H * W1, W2 >> l, pyramid_dtype))
+            if too_big:
+                warnings.warn(f"CorrBlock1D: shadow copies of levels {too_big} dropped: a level "
+                              "plus its copy exceeds the pair kernel's 4 GiB window", stacklevel=2)
+                self._shadow = self._shadow - frozenset(too_big)
+            # exact_f32: the exact fp32 MFMA volume kernel instead of the
+            # split-bf16 default (both fp32-accurate)
             self._levels = build_pyramid(fmap1, fmap2, nbuf, pyramid_dtype, skip=skip,
-                                         shadow=self._shadow)
+                                         shadow=self._shadow, exact_f32=exact_f32)
             self._levels += [None] * (num_levels + 1 - nbuf)
         self._state = self._token = None
         if grad:
@@ -671,9 +704,9 @@ class CorrBlock1D:
                              bias, relu)
 
     @staticmethod
-    def corr(fmap1, fmap2):
+    def corr(fmap1, fmap2, exact_f32=False):
         B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
-        lvl0 = build_pyramid(fmap1, fmap2, 1, pad=False)[0]
+        lvl0 = build_pyramid(fmap1, fmap2, 1, pad=False, exact_f32=exact_f32)[0]
         return lvl0.view(B, H, W1, 1, W2)
 
 

@@ -34,6 +34,19 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // RC_SHADOW (ABI v5): byte offset from a stored level's base to its copy.
 long long shadow_offset(long long rows, long long ld, int esize) { return RC_SHADOW_OFFSET(rows, ld, esize); }
 
+// pyr_dtype bits an entry point accepts: the element type (low byte), the
+// RC_SHADOW_LEVEL bits and, where the pair kernel serves it, RC_OUT_CHANNELS_LAST.
+int check_flags(const char *who, int pyr_dtype, bool allow_cl, bool build = false) {
+    const unsigned known = 0xFFu | RC_SHADOW | (allow_cl ? (unsigned)RC_OUT_CHANNELS_LAST : 0u) |
+                           (build ? (unsigned)RC_BUILD_EXACT_F32 : 0u);
+    if (!allow_cl && (pyr_dtype & RC_OUT_CHANNELS_LAST))
+        return fail(RC_EUNSUPPORTED, "%s: RC_OUT_CHANNELS_LAST is only defined for "
+                    "rc_corr_lookup_chain / rc_corr_lookup_step", who);
+    if ((unsigned)pyr_dtype & ~known)
+        return fail(RC_EINVAL, "%s: unknown pyr_dtype flag bits 0x%x", who, (unsigned)pyr_dtype & ~known);
+    return RC_OK;
+}
+
 bool is_pow2_float(float v) {
     int e;
     return std::frexp(v, &e) == 0.5f;
@@ -57,6 +70,8 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
                              int H, int W1, int W2, void *const *pyr, const long *pyr_ld, int nbuf,
                              int pyr_dtype, void *stream) {
     g_err[0] = 0;
+    if (int e = check_flags("rc_corr_build", pyr_dtype, false, true)) return e;
+    const bool exact_f32 = (pyr_dtype & RC_BUILD_EXACT_F32) != 0;
     const unsigned shmask = ((unsigned)pyr_dtype >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits
     pyr_dtype &= 0xFF;
     if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
@@ -114,9 +129,14 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     // fp32 fmaps + fp32 pyramid: exact fp32 MFMA.  bf16 fmaps, or a bf16
     // pyramid (bf16-level tolerance requested), take the bf16 MFMA kernel.
     const bool bf16_mma = fmap_dtype == RC_BF16 || pyr_dtype == RC_BF16;
-    int rc = hip_rc(bf16_mma ? rc_launch_build_bf16mma(a, fmap_dtype == RC_BF16, s)
-                             : rc_launch_build_f32(a, s),
-                    "rc_corr_build: volume launch");
+    // fp32: the split-bf16 kernel (fp32 accuracy, volume_split.hip) unless the
+    // exact fp32 MFMA kernel is asked for or the shape is outside the split
+    // kernel's addressing (hipErrorNotSupported: nothing was launched)
+    hipError_t e = hipErrorNotSupported;
+    if (bf16_mma) e = rc_launch_build_bf16mma(a, fmap_dtype == RC_BF16, s);
+    else if (!exact_f32) e = rc_launch_build_split(a, s);
+    if (e == hipErrorNotSupported && !bf16_mma) e = rc_launch_build_f32(a, s);
+    int rc = hip_rc(e, "rc_corr_build: volume launch");
     if (rc) return rc;
     const long rows = (long)B * H * W1;
     for (int l = a.nfused; l < nbuf; ++l) {
@@ -138,6 +158,7 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
 extern "C" int rc_corr_pool(const void *in, long ld_in, void *out, long ld_out, long rows,
                             int W_in, int dtype, void *stream) {
     g_err[0] = 0;
+    if (int e = check_flags("rc_corr_pool", dtype, false)) return e;
     dtype &= 0xFF;    // pools the primary copy; a shadow is not written
     if (rows < 0 || W_in < 2 || ld_in < W_in || ld_out < W_in / 2)
         return fail(RC_EINVAL, "rc_corr_pool: bad shape rows=%ld W_in=%d ld_in=%ld ld_out=%ld", rows,
@@ -260,6 +281,7 @@ extern "C" int rc_corr_lookup(const void *const *pyr, const int *widths, const l
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
+    if (int e = check_flags("rc_corr_lookup", pyr_dtype, false)) return e;
     int rc = prep_lookup("rc_corr_lookup", pyr, widths, pyr_ld, pyr_dtype, levels, radius, coords_x,
                          coord_batch_stride, B, H, W1, out, a, &empty);
     if (rc || empty) return rc;
@@ -277,6 +299,7 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
+    if (int e = check_flags("rc_corr_lookup_chain", pyr_dtype, true)) return e;
     int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty, true);
     if (rc) return rc;
@@ -307,6 +330,7 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
+    if (int e = check_flags("rc_corr_lookup_step", pyr_dtype, true)) return e;
     int rc = prep_lookup("rc_corr_lookup_step", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords1, 2L * H * W1, B, H, W1, out, a, &empty, chain != 0);
     if (rc || empty) return rc;
@@ -473,6 +497,7 @@ extern "C" int rc_corr_lookup_conv(const void *const *pyr, const int *widths, co
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
+    if (int e = check_flags("rc_corr_lookup_conv", pyr_dtype, false)) return e;
     int rc = prep_lookup("rc_corr_lookup_conv", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty);
     if (rc) return rc;

@@ -1,0 +1,246 @@
+// Epilogue helpers shared by the volume kernels (volume.hip,
+// volume_split.hip): scaled level values -> pyramid memory, including the
+// swapped-operand epilogue that pools levels 1-2 lane-locally and stages
+// each level through a wave-private LDS image for whole-row stores.
+#pragma once
+#include "common.h"
+
+namespace rc {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Dev-only ablation flags (RAFTCORR_BUILD_MODE): 1 = no operand loads,
+// 2 = no epilogue stores.  Product launches use 0.
+enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8, kModeNoFragReads = 16,
+       kModeStagger = 64 };
+
+// VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
+template <int VW>
+__device__ __forceinline__ void store_vec1(void *lvl, bool bf16, long long g, const float *v) {
+    if (bf16) {
+        uint16_t *d = reinterpret_cast<uint16_t *>(lvl) + g;
+        if constexpr (VW == 1) {
+            d[0] = f32_to_bf16(v[0]);
+        } else {
+            unsigned w[VW / 2];
+#pragma unroll
+            for (int k = 0; k < VW / 2; ++k)
+                w[k] = (unsigned)f32_to_bf16(v[2 * k]) | ((unsigned)f32_to_bf16(v[2 * k + 1]) << 16);
+            if constexpr (VW == 8) *reinterpret_cast<uint4 *>(d) = uint4{w[0], w[1], w[2], w[3]};
+            else if constexpr (VW == 4) *reinterpret_cast<uint2 *>(d) = uint2{w[0], w[1]};
+            else *reinterpret_cast<unsigned *>(d) = w[0];
+        }
+    } else {
+        float *d = reinterpret_cast<float *>(lvl) + g;
+        if constexpr (VW >= 4) {
+#pragma unroll
+            for (int k = 0; k < VW; k += 4)
+                *reinterpret_cast<f32x4 *>(d + k) = f32x4{v[k], v[k + 1], v[k + 2], v[k + 3]};
+        } else if constexpr (VW == 2) {
+            *reinterpret_cast<f32x2 *>(d) = f32x2{v[0], v[1]};
+        } else {
+            d[0] = v[0];
+        }
+    }
+}
+
+// ... and to the level's line-phase shadow copy at +sh bytes when sh != 0
+// (RC_SHADOW: the same values, every store duplicated; sh is wave-uniform).
+template <int VW>
+__device__ __forceinline__ void store_vec(void *lvl, bool bf16, long long g, const float *v, long long sh) {
+    store_vec1<VW>(lvl, bf16, g, v);
+    if (sh) store_vec1<VW>(static_cast<char *>(lvl) + sh, bf16, g, v);
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+    return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)(p);
+}
+
+// The epilogue's wave-private staging accesses are inline asm too (see
+// tr_read_asm): in-order LDS execution within a wave orders them, and a
+// read's result is used only after the lgkmcnt(0) wait inside its asm.
+__device__ __forceinline__ void lds_st4(uint32_t a, f32x4 v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v));
+}
+__device__ __forceinline__ void lds_st2(uint32_t a, f32x2 v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v));
+}
+__device__ __forceinline__ void lds_st1(uint32_t a, float v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v));
+}
+
+// Rows [0, 16) of a wave's staged level image (fp32 at LDS address st,
+// pitch p floats, cw columns) -> level memory, VW elements per lane, cw / VW
+// lanes per row.
+template <int VW>
+__device__ __forceinline__ void store_rows16(uint32_t st, int p, int cw, void *lvl, long long ld,
+                                             bool bf16, long long rowbase, int w1_0, int col0, int W1,
+                                             int Wl, int lane, long long sh) {
+    const int lpr = cw / VW;                 // lanes per row
+    const int rpi = 64 / lpr;                // rows per instruction
+    const int Rl = lane / lpr, j = (lane - Rl * lpr) * VW;
+    const int col = col0 + j;
+    for (int r0 = 0; r0 < 16; r0 += rpi) {
+        const int R = r0 + Rl, w1 = w1_0 + R;
+        const uint32_t src = st + 4 * (R * p + j);
+        float v[VW];
+        if constexpr (VW == 8) {
+            f32x4 x0, x1;
+            asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(x0), "=&v"(x1) : "v"(src));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) { v[c] = x0[c]; v[4 + c] = x1[c]; }
+        } else if constexpr (VW == 4) {
+            f32x4 x0;
+            asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x0) : "v"(src));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = x0[c];
+        } else if constexpr (VW == 2) {
+            f32x2 x0;
+            asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x0) : "v"(src));
+            v[0] = x0[0]; v[1] = x0[1];
+        } else {
+            float x0;
+            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x0) : "v"(src));
+            v[0] = x0;
+        }
+        const bool ok = Rl < rpi && R < 16 && w1 < W1 && col < Wl;
+        if (ok) store_vec<VW>(lvl, bf16, (rowbase + w1) * ld + col, v, sh);
+    }
+}
+
+__device__ __forceinline__ void store_rows16_any(uint32_t st, int p, int cw, void *lvl, long long ld,
+                                                 bool bf16, long long rowbase, int w1_0, int col0,
+                                                 int W1, int Wl, int lane, long long sh) {
+    // widest vector dividing the image width (col0 is a multiple of it) and
+    // the row stride
+    if (bf16 && ld % 8 == 0 && cw % 8 == 0)
+        store_rows16<8>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
+    else if (ld % 4 == 0 && cw % 4 == 0)
+        store_rows16<4>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
+    else if (ld % 2 == 0 && cw % 2 == 0)
+        store_rows16<2>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
+    else
+        store_rows16<1>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
+}
+
+__device__ __forceinline__ float pool2(float x, float y, bool bf) {
+    const float m = (x + y) * 0.5f;
+    return bf ? round_bf16(m) : m;
+}
+
+// Epilogue of the swapped-operand tile: acc[ma][nb] register r of lane l =
+// C[w1 = m0 + 16nb + (l&15)][w2 = n0 + 16ma + 4(l>>4) + r].  One fragment
+// column nb (16 w1 rows) at a time, every level: level l's image has rows
+// w1 - m0 - 16nb, columns (w2 - n0) >> l, pitch (WT >> l) + 4 floats.
+template <int FMA, int MODE, int NLM>
+__device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const BuildArgs &a, int row,
+                                                 int m0, int n0, int lane0, uint32_t st0) {
+    constexpr int WT = 16 * FMA;
+    const bool bf = a.pyr_bf16 != 0;
+    const long long rowbase = (long long)row * a.W1;
+    const int nl = a.nfused < NLM ? a.nfused : NLM;
+    // one loop body for the four columns (code size, registers): column nb
+    // is always acc[.][0], the others move down one per pass
+#pragma unroll 1
+    for (int nb = 0; nb < 4; ++nb) {
+        // opaque per pass: otherwise the compiler hoists the per-lane staging
+        // and store addresses of every level and vector width out of the
+        // loops and keeps ~100 of them in VGPRs
+        int lane = lane0;
+        uint32_t st = st0;
+        asm volatile("" : "+v"(lane), "+v"(st));
+        const int g = lane >> 4, i = lane & 15;
+        auto flush = [&](int l) {
+            const int cw = WT >> l;
+            store_rows16_any(st, cw + 4, cw, a.lvl[l], a.ld[l], bf, rowbase, m0 + 16 * nb, n0 >> l, a.W1,
+                             a.W2 >> l, lane, a.shadow[l]);
+        };
+        float v[FMA][4];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float x = acc[ma][0][r];
+                const float c = a.pow2 ? x * a.scale : x / a.sq;
+                v[ma][r] = bf ? round_bf16(c) : c;
+            }
+            acc[ma][0] = acc[ma][1];
+            acc[ma][1] = acc[ma][2];
+            acc[ma][2] = acc[ma][3];
+        }
+        if constexpr (MODE & kModeNoStores) {
+            float keep = 0.f;
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma) keep += v[ma][0] + v[ma][3];
+            asm volatile("" ::"v"(keep));
+            continue;
+        }
+        if (a.lvl[0]) {
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma)
+                lds_st4(st + 4 * (i * (WT + 4) + 16 * ma + 4 * g), f32x4{v[ma][0], v[ma][1], v[ma][2], v[ma][3]});
+            flush(0);
+        }
+        if (nl < 2) continue;
+        // level 1: lane-local pairs of w2
+        float u[FMA][2];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+            u[ma][0] = pool2(v[ma][0], v[ma][1], bf);
+            u[ma][1] = pool2(v[ma][2], v[ma][3], bf);
+        }
+        if (a.lvl[1]) {
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma)
+                lds_st2(st + 4 * (i * (WT / 2 + 4) + 8 * ma + 2 * g), f32x2{u[ma][0], u[ma][1]});
+            flush(1);
+        }
+        if (nl < 3) continue;
+        // level 2: lane-local
+        float s2[FMA];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) s2[ma] = pool2(u[ma][0], u[ma][1], bf);
+        if (a.lvl[2]) {
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma) lds_st1(st + 4 * (i * (WT / 4 + 4) + 4 * ma + g), s2[ma]);
+            flush(2);
+        }
+        if (nl < 4) continue;
+        // level 3: lanes l, l^16 (w2 groups g, g^1); the even-g lane stores it
+        float s3[FMA];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+            const float o = __shfl_xor(s2[ma], 16);
+            s3[ma] = (g & 1) ? pool2(o, s2[ma], bf) : pool2(s2[ma], o, bf);
+        }
+        if (a.lvl[3]) {
+            if (!(g & 1)) {
+#pragma unroll
+                for (int ma = 0; ma < FMA; ++ma) lds_st1(st + 4 * (i * (WT / 8 + 4) + 2 * ma + (g >> 1)), s3[ma]);
+            }
+            flush(3);
+        }
+        if (nl < 5) continue;
+        // level 4: lanes l, l^32 (g = 0 with g = 2)
+        float s4[FMA];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+            const float o = __shfl_xor(s3[ma], 32);
+            s4[ma] = (g & 2) ? pool2(o, s3[ma], bf) : pool2(s3[ma], o, bf);
+        }
+        if (a.lvl[4]) {
+            if (g == 0) {
+#pragma unroll
+                for (int ma = 0; ma < FMA; ++ma) lds_st1(st + 4 * (i * (WT / 16 + 4) + ma), s4[ma]);
+            }
+            flush(4);
+        }
+    }
+}
+
+}  // namespace rc

@@ -1,0 +1,265 @@
+// fp32 correlation volume on bf16 MFMA by a three-way split of every operand
+// (gfx950) -- the default fp32 build since ABI v6.
+//
+// Replaces CorrBlock1D.corr (/root/reference/model.py:318-326) and the
+// avg_pool2d loop of CorrBlock1D.__init__ (:284-295), like the exact fp32
+// MFMA kernel of volume.hip, at fp32 accuracy for a third of its MFMA time.
+//
+// Each fp32 operand x is cut into three bf16 pieces, x = h + m + l EXACTLY
+// (h = RN_bf16(x), m = RN_bf16(x - h), l = RN_bf16(x - h - m); every
+// subtraction is exact, and 3 x 8 significant bits plus the two sign bits the
+// round-to-nearest steps gain cover fp32's 24).  Per 32-deep K step the
+// product of two operands is the sum of six bf16 MFMAs,
+//     mm + hl + lh + hm + mh + hh   (v_mfma_f32_16x16x32_bf16, fp32 accumulate)
+// which drops only ml, lm, ll: below 2^-27 of |a||b| per product, under the
+// fp32 rounding of the accumulation itself.  Measured against the fp64 oracle
+// it is as accurate as the fp32 MFMA chain (tests/test_split_gpu.py).  bf16
+// MFMA runs 16x the fp32 MFMA rate, so six of them cost 3/8 of the fp32 MFMA
+// time; the build becomes bound by HBM (fmaps in, pyramid out) instead of by
+// the fp32 matrix rate.
+//
+// Non-finite fmap values: an inf operand splits into inf and NaN pieces, so
+// an inf in a row gives NaN where an fp32 GEMM gives +-inf (a NaN stays NaN);
+// |x| > 3.39e38 rounds its bf16 head to inf.  RC_BUILD_EXACT_F32 selects the
+// exact fp32 MFMA kernel for such inputs.
+//
+// Workgroup: 256 threads = 4 waves as 2 x 2 wave tiles of 64 (w2) x 64 (w1)
+// (swapped operands: A = F2 rows -> M = w2, B = F1 rows -> N = w1, so every
+// lane's accumulators hold 4 consecutive w2 of one w1 row and pyramid levels
+// 1-2 pool lane-locally -- the epilogue of the bf16 ring kernel,
+// epilogue_swapped).  Operand staging is the fp32 kernel's LDS-DMA ring
+// (volume.hip): 16-d stages of [16 d][128 w] fp32 for F1 and for F2, filled
+// by buffer_load ... lds with no VGPR staging, SL slots, one K step (32 d =
+// two stages) multiplied while the next is in flight.  Each DMA instruction
+// lands two 512-B rows; the blocks are 1040 B apart (16 B of padding) so the
+// two 16-lane halves of a fragment read (rows 8 apart) fall on different
+// banks.  Fragments are read in fp32 (lane (i, g): 8 consecutive d at one w,
+// eight ds_read_b32 with immediate offsets) and split in registers right
+// before their MFMAs.  Fragments (16 w) that lie wholly beyond W1 / W2 are
+// skipped (template FA / FB), so W = 240 wastes no MFMA work.
+#include "common.h"
+#include "epilogue.h"
+
+namespace rc {
+
+constexpr int kSpBK = 16;                   // d per ring stage (two per K step)
+constexpr int kSpBlk = 1040;                // bytes per DMA block: 2 rows of 128 fp32 + 16 B pad
+constexpr int kSpOp = 8 * kSpBlk;           // one operand tile of a stage: 16 rows
+constexpr int kSpSlot = 2 * kSpOp;          // F1 + F2
+constexpr int kSpSL = 4;                    // ring slots (stages): one K step in flight, one in use
+constexpr int kSpMaxFused = 5;              // levels the epilogue writes (more: pooled from memory)
+constexpr int kSpStb = 16 * (64 + 4) * 4;   // per-wave epilogue staging (epilogue_swapped, WT 64)
+static_assert(4 * kSpStb <= kSpSL * kSpSlot, "epilogue staging aliases the ring");
+
+typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+typedef __bf16 sp_bf16x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> packed bf16 (RNE), and back to fp32
+__device__ __forceinline__ uint32_t sp_pack(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, sp_bf16x2));   // v_cvt_pk_bf16_f32
+}
+__device__ __forceinline__ float sp_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float sp_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xFFFF0000u); }
+
+struct SplitFrag {
+    bf16x8 h, m, l;
+};
+
+// 8 consecutive d of one w -> head, middle and low bf16 pieces (each exact
+// residual of the previous: x = h + m + l for finite |x| < 3.39e38).
+__device__ __forceinline__ SplitFrag sp_split(const float (&x)[8]) {
+    u32x4s h, m, l;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t hp = sp_pack(x[2 * k], x[2 * k + 1]);
+        const float r0 = x[2 * k] - sp_lo(hp), r1 = x[2 * k + 1] - sp_hi(hp);      // exact
+        const uint32_t mp = sp_pack(r0, r1);
+        const float s0 = r0 - sp_lo(mp), s1 = r1 - sp_hi(mp);                      // exact
+        h[k] = hp;
+        m[k] = mp;
+        l[k] = sp_pack(s0, s1);
+    }
+    return SplitFrag{__builtin_bit_cast(bf16x8, h), __builtin_bit_cast(bf16x8, m), __builtin_bit_cast(bf16x8, l)};
+}
+
+// One lane's fragment: rows r0..r0+7 (d inside the stage) of w column w of an
+// operand tile at LDS byte address base.  Row d of the tile sits in block
+// d >> 1 at +512 B for odd d.
+template <int MODE>
+__device__ __forceinline__ SplitFrag sp_read(const char *base) {
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = *reinterpret_cast<const float *>(base + (j >> 1) * kSpBlk + (j & 1) * 512);
+    return sp_split(x);
+}
+
+struct SpCtx {
+    __amdgpu_buffer_rsrc_t r1, r2;
+    int D, H, h, W1, W2, M0, N0, wave, lane, nst;
+};
+
+// DMA share of this wave per stage: rows 4w..4w+3 of both tiles, 2 rows
+// (1 KB = 64 lanes x 16 B) per instruction -> 4 instructions per stage.
+template <int MODE>
+__device__ __forceinline__ void sp_issue(const SpCtx &c, char *smem, int st) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    char *sA = smem + (st % kSpSL) * kSpSlot, *sB = sA + kSpOp;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r0 = 4 * c.wave + 2 * i;
+        const int d = st * kSpBK + r0 + (c.lane >> 5);
+        const int w = 4 * (c.lane & 31);
+        const long long base = (long long)(d < c.D ? d : 0) * c.H + c.h;
+        const uint32_t offA = d < c.D ? (uint32_t)((base * c.W1 + c.M0 + w) * 4) : 0xFFFFFF00u;
+        const uint32_t offB = d < c.D ? (uint32_t)((base * c.W2 + c.N0 + w) * 4) : 0xFFFFFF00u;
+        if constexpr (!(MODE & kModeNoLoads)) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r1, (lds_void *)(sA + (r0 >> 1) * kSpBlk), 16, (int)offA, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r2, (lds_void *)(sB + (r0 >> 1) * kSpBlk), 16, (int)offB, 0, 0, 0);
+        }
+    }
+}
+
+// K loop + epilogue of one wave with FA valid A fragments (w2) and FB valid B
+// fragments (w1); FA = 0: no valid columns -- the wave still issues its DMA
+// share and joins every barrier.
+template <int FA, int FB, int MODE, int NLM>
+__device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, char *smem, int row) {
+    const int wm = c.wave & 1, wn = c.wave >> 1;         // w1 half (B), w2 half (A)
+    const int lane = c.lane, i = lane & 15, g = lane >> 4;
+    // lane (i, g) reads d rows 8(g & 1) .. +7 of stage (g >> 1) of the K step
+    const int lrow = (g & 1) * 4 * kSpBlk;               // rows 8(g&1): 4 blocks in
+    f32x4 acc[FA > 0 ? FA : 1][4];
+#pragma unroll
+    for (int x0 = 0; x0 < (FA > 0 ? FA : 1); ++x0)
+#pragma unroll
+        for (int y0 = 0; y0 < 4; ++y0) acc[x0][y0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nks = (c.nst + 1) >> 1;                     // K steps (the launcher pads nst to even)
+    // stages of K steps 0 and 1 in flight
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+        if (st < c.nst) sp_issue<MODE>(c, smem, st);
+    for (int ks = 0; ks < nks; ++ks) {
+        // RAW: my 8 DMA instructions of K step ks landed (K step 1, issued
+        // with K step 0 before the loop, may still fly at ks = 0; later K
+        // steps are issued after this wait); WAR: my LDS reads of K step
+        // ks - 1 are done.  Barrier.
+        if (ks == 0 && nks > 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (ks >= 1 && 2 * ks + 2 < c.nst) {             // K step ks + 1 into the slots of K step ks - 1
+            sp_issue<MODE>(c, smem, 2 * ks + 2);
+            sp_issue<MODE>(c, smem, 2 * ks + 3);
+        }
+        if constexpr (FA > 0 && !(MODE & kModeNoMath)) {
+            const char *st = smem + ((2 * ks + (g >> 1)) % kSpSL) * kSpSlot + lrow;
+            const char *pb = st + 4 * (64 * wm + i);                     // F1 (B): this wave's w1
+            const char *pa = st + kSpOp + 4 * (64 * wn + i);             // F2 (A): this wave's w2
+            SplitFrag fb[FB];
+#pragma unroll
+            for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE>(pb + 64 * n);
+#pragma unroll
+            for (int m = 0; m < FA; ++m) {
+                const SplitFrag fa = sp_read<MODE>(pa + 64 * m);
+#pragma unroll
+                for (int n = 0; n < FB; ++n) {
+                    // small terms first (the six leading products of h+m+l)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.m, fb[n].m, acc[m][n], 0, 0, 0);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.h, fb[n].l, acc[m][n], 0, 0, 0);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.l, fb[n].h, acc[m][n], 0, 0, 0);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.h, fb[n].m, acc[m][n], 0, 0, 0);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.m, fb[n].h, acc[m][n], 0, 0, 0);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.h, fb[n].h, acc[m][n], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // the ring becomes the waves' epilogue staging images
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if constexpr (FA > 0)
+        epilogue_swapped<FA, MODE, NLM>(acc, a, row, c.M0 + 64 * wm, c.N0 + 64 * wn, lane,
+                                        lds_u32(smem + c.wave * kSpStb));
+}
+
+template <int FA, int MODE, int NLM>
+__device__ __forceinline__ void split_fb(int fb, const SpCtx &c, const BuildArgs &a, char *smem, int row) {
+    if (fb >= 4) split_body<FA, 4, MODE, NLM>(c, a, smem, row);
+    else if (fb == 3) split_body<FA, 3, MODE, NLM>(c, a, smem, row);
+    else if (fb == 2) split_body<FA, 2, MODE, NLM>(c, a, smem, row);
+    else split_body<FA, 1, MODE, NLM>(c, a, smem, row);
+}
+
+template <int MODE, int NLM>
+__global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nwg_total) {
+    __shared__ __attribute__((aligned(16))) char smem[kSpSL * kSpSlot];
+    SpCtx c;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.lane = threadIdx.x & 63;
+    const int T = a.tiles_m * a.tiles_n;
+    const int wgid = xcd_remap(blockIdx.x, nwg_total);   // a row's tiles share an XCD (and its L2)
+    const int row = wgid / T, tile = wgid - row * T;
+    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int b = row / a.H;
+    c.h = row - b * a.H;
+    c.D = a.D; c.H = a.H; c.W1 = a.W1; c.W2 = a.W2;
+    c.M0 = tm * 128; c.N0 = tn * 128;
+    c.nst = 2 * ((a.D + 2 * kSpBK - 1) / (2 * kSpBK));   // whole K steps (d >= D reads zeros)
+    const long long img1 = (long long)a.D * a.H * a.W1, img2 = (long long)a.D * a.H * a.W2;
+    c.r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
+    c.r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
+    // valid 16-wide fragments of this wave's 64 x 64 tile (wave-uniform)
+    const int cw2 = a.W2 - (c.N0 + 64 * (c.wave >> 1)), cw1 = a.W1 - (c.M0 + 64 * (c.wave & 1));
+    const int fa = cw2 <= 0 || cw1 <= 0 ? 0 : (cw2 >= 64 ? 4 : (cw2 + 15) >> 4);
+    const int fb = cw1 >= 64 ? 4 : (cw1 + 15) >> 4;
+    if (fa == 4) split_fb<4, MODE, NLM>(fb, c, a, smem, row);
+    else if (fa == 3) split_fb<3, MODE, NLM>(fb, c, a, smem, row);
+    else if (fa == 2) split_fb<2, MODE, NLM>(fb, c, a, smem, row);
+    else if (fa == 1) split_fb<1, MODE, NLM>(fb, c, a, smem, row);
+    else split_body<0, 1, MODE, NLM>(c, a, smem, row);
+}
+
+}  // namespace rc
+
+// Split-bf16 build for fp32 fmaps and an fp32 pyramid.  Returns
+// hipErrorNotSupported (nothing launched) when the shape is outside what the
+// kernel addresses; the caller then runs the exact fp32 MFMA kernel.  Fuses
+// at most kSpMaxFused levels: a.nfused is lowered to what was written
+// and the caller pools the rest.
+hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
+    // per-image byte offsets are 32-bit (0xFFFFFF00 = the out-of-range marker),
+    // and rows are DMA'd in 16-B pieces (W1, W2 multiples of 4)
+    const long long img = (long long)a.D * a.H * (a.W1 > a.W2 ? a.W1 : a.W2) * 4;
+    if (img >= 0xFFFFFF00LL || a.pyr_bf16 || a.W1 % 4 || a.W2 % 4) return hipErrorNotSupported;
+    if (a.nfused > rc::kSpMaxFused) {
+        // levels past the fused ones are pooled from memory: they must exist
+        for (int l = rc::kSpMaxFused - 1; l < a.nfused; ++l)
+            if (!a.lvl[l]) return hipErrorNotSupported;
+        a.nfused = rc::kSpMaxFused;
+    }
+    const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
+    if (nwg <= 0) return hipSuccess;
+    if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
+#ifdef RAFTCORR_DEV
+    // dev-only ablations (timing only): RAFTCORR_SPLIT_MODE = kMode* flags
+    // (1 no operand loads, 2 no epilogue stores, 4 no MFMAs; sums combine)
+    switch (rc::dev_knob("RAFTCORR_SPLIT_MODE")) {
+        case 1: hipLaunchKernelGGL((rc::build_split_kernel<1, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
+        case 2: hipLaunchKernelGGL((rc::build_split_kernel<2, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
+        case 3: hipLaunchKernelGGL((rc::build_split_kernel<3, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
+        case 4: hipLaunchKernelGGL((rc::build_split_kernel<4, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
+        case 6: hipLaunchKernelGGL((rc::build_split_kernel<6, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
+        case 7: hipLaunchKernelGGL((rc::build_split_kernel<7, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
+        default: break;
+    }
+#endif
+    // up to 3 fused levels (the pair layout: 0 and 2 stored) keeps the
+    // epilogue's level pointers out of the scalar registers
+    if (a.nfused <= 3)
+        hipLaunchKernelGGL((rc::build_split_kernel<0, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg);
+    else
+        hipLaunchKernelGGL((rc::build_split_kernel<0, rc::kSpMaxFused>), dim3((unsigned)nwg), dim3(256), 0, s, a,
+                           (int)nwg);
+    return hipGetLastError();
+}

@@ -150,8 +150,10 @@ class RowShardedStereo:
       features equal the full-image ones.  cnet's BatchNorms run on running stats in
       eval mode (per pixel); conv2's two InstanceNorms (model.py:35-39, :345)
       take image-wide statistics through one all-reduce each
-      (``_instance_norm_rows``).  ``shard_encoders=False`` runs the encoders
-      replicated on the full image (no exchange; redundant encoder FLOPs).
+      (``_instance_norm_rows``).  ``shard_encoders=False`` -- and any model
+      in train mode, whose BatchNorms need batch statistics of the whole
+      image -- runs the encoders replicated on the full image (no exchange;
+      redundant encoder FLOPs).
     * Rank k owns 1/4-res feature rows [r0, r1) (multiples of 4) and keeps GRU
       state for the extended slab [r0 - halo, r1 + halo) (1/8 and 1/16 res:
       halo/2, halo/4).  The correlation pyramid is built for the slab's rows
@@ -164,13 +166,20 @@ class RowShardedStereo:
       res are exact to rounding (gloo, 3 ranks: 1.9e-6 px max; 8 rows
       5.7e-6; 4 rows 8.8e-3).  ``per_stage=False`` exchanges every level once
       per iteration and needs a halo covering the whole iteration's cone
-      (<= 20 rows; 24-32 used).
+      (<= 20 rows): ``halo`` defaults to 12 / 24 rows by mode, and a halo
+      below 20 rows with ``per_stage=False`` raises ValueError.
     * ``forward`` returns the per-iteration flow of the OWNED rows;
       ``gather_rows`` assembles full-height tensors.
     """
 
-    def __init__(self, model, rank, world, halo=12, group=None, shard_encoders=True, enc_margin=48,
+    def __init__(self, model, rank, world, halo=None, group=None, shard_encoders=True, enc_margin=48,
                  per_stage=True):
+        # one stage's cone needs 12 rows; a whole iteration's up to 20 (SURVEY §8e)
+        if halo is None:
+            halo = 12 if per_stage else 24
+        if not per_stage and halo < 20:
+            raise ValueError(f"halo={halo} < 20 rows: with per_stage=False the halo must cover "
+                             "one whole iteration's dependency cone (SURVEY.md §8e)")
         if halo % 4:
             raise ValueError("halo must be a multiple of 4")
         if enc_margin % 4:
@@ -290,7 +299,9 @@ class RowShardedStereo:
     def forward(self, image1, image2, iters=12):
         m, a = self.model, self.model.args
         nl = a.n_gru_layers
-        if self.shard_encoders:
+        # train-mode BatchNorm needs the whole image's batch statistics: the
+        # replicated encoders give exactly the unsharded network's features
+        if self.shard_encoders and not m.training:
             glob = self._heights(image1.shape[2], a.n_downsample, nl)
             H1 = glob[0]
             r0, r1, e0, e1 = self._ranges(H1)

@@ -150,3 +150,29 @@ def test_grad_shadow_flag_validation():
         rcorr.grad_buffers(16, [64, 32], "cpu", pair=True, shadow=(0,))
     with pytest.raises(ValueError):
         rcorr.grad_buffers(16, [64, 32, 16, 8], "cpu", pair=True, shadow=(1,))
+
+
+def test_pyr_dtype_flag_bits_validated():
+    """RC_OUT_CHANNELS_LAST on an entry point that cannot honour it
+    is refused (RC_EUNSUPPORTED), and unknown flag bits are RC_EINVAL, on every
+    entry point that takes a pyr_dtype -- before any launch."""
+    L = _lib.lib()
+    f = lambda a: ctypes.c_void_p(a)  # noqa: E731
+    ptrs = _lib.ptr_array([f(0x1000)])
+    w = _lib.int_array([8])
+    cl = _lib.RC_F32 | _lib.RC_OUT_CHANNELS_LAST
+    junk = _lib.RC_F32 | 0x400000
+    for dt, code in ((cl, _lib.RC_EUNSUPPORTED), (junk, _lib.RC_EINVAL)):
+        assert L.rc_corr_lookup(ptrs, w, None, dt, 1, 4, f(0x2000), 0, 1, 1, 8, f(0x3000), None) == code
+        assert L.rc_corr_lookup_conv(ptrs, w, None, dt, 1, 4, f(0x2000), 0, 1, 1, 8, f(0x4000), None, 4,
+                                     1, f(0x3000), None) == code
+        assert _build(pdt=dt, B=0) == code
+        assert L.rc_corr_pool(None, 8, None, 4, 0, 8, dt, None) == code
+        assert L.rc_last_error()
+    two = _lib.ptr_array([f(0x1000), None])
+    w2 = _lib.int_array([64, 32])
+    for fn in ("rc_corr_lookup_chain",):
+        assert getattr(L, fn)(two, w2, None, junk, 2, 4, f(0x2000), 0, 1, 1, 64, f(0x3000),
+                              None) == _lib.RC_EINVAL
+    assert L.rc_corr_lookup_step(two, w2, None, junk, 2, 4, 1, f(0x2000), None, f(0x3000), f(0x5000),
+                                 1, 1, 64, f(0x4000), None) == _lib.RC_EINVAL

@@ -21,3 +21,23 @@ def test_coords_grid_matches_reference_layout():
     assert g.shape == (2, 2, 3, 5) and g.dtype == torch.float32
     assert torch.equal(g[1, 0, 2], torch.arange(5).float())
     assert torch.equal(g[0, 1, :, 4], torch.arange(3).float())
+
+
+def test_request_validation_before_any_launch():
+    """invalid ``grad_shadow`` requests raise at construction (not
+    later inside autograd), a ``per_stage=False`` halo below the one-iteration
+    cone raises, and the default halo follows the exchange mode."""
+    from raft_stereo_amd import corr as rcorr
+    from raft_stereo_amd.shard import RowShardedStereo
+    with pytest.raises(ValueError):
+        rcorr._check_grad_shadow((1,), 4, 4, 240)
+    with pytest.raises(ValueError):
+        rcorr._check_grad_shadow((0,), 3, 4, 240)        # 3 levels: no pair gradient layout
+    with pytest.raises(ValueError):
+        rcorr._check_grad_shadow((0, 2), 4, 5, 240)      # radius 5: per-level layout
+    rcorr._check_grad_shadow((0, 2), 4, 4, 240)
+    rcorr._check_grad_shadow((), 3, 4, 240)
+    with pytest.raises(ValueError):
+        RowShardedStereo(None, 0, 2, halo=12, per_stage=False)
+    assert RowShardedStereo(None, 0, 2).halo == 12
+    assert RowShardedStereo(None, 0, 2, per_stage=False).halo == 24

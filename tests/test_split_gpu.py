@@ -1,0 +1,109 @@
+"""The split-bf16 fp32 volume (csrc/volume_split.hip, the fp32 default since
+ABI v6) against the C oracle's fp64 volume and against the exact fp32 MFMA
+kernel (RC_BUILD_EXACT_F32) -- model.py:318-326 (volume) and :284-295
+(pyramid).
+
+Bar (SURVEY §8d fp32 contract): max|d|/max|ref| <= 1e-4 and rel-L2 <= 1e-5
+per tensor.  The split kernel is also held to the exact kernel's own error:
+its error against fp64 must not exceed twice the fp32 MFMA kernel's (or
+1e-6), i.e. it is an fp32-accurate volume, not a reduced-precision one.
+Pooled levels are bit-exact from the level below (avg_pool2d's fp32 ops).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import norm_err, rel_l2, same
+from oracle import coracle
+from raft_stereo_amd import CorrBlock1D
+from raft_stereo_amd import corr as rcorr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+SHAPES = [
+    # B, D, H, W1, W2
+    (2, 256, 3, 240, 240),      # config 2 rows: fragment tails at 240
+    (1, 256, 2, 160, 160),      # config 5 rows
+    (1, 256, 2, 720, 720),      # config 4 rows
+    (1, 256, 2, 311, 311),      # odd width, not a multiple of 4
+    (2, 40, 3, 37, 45),         # D % 32 != 0, W1 != W2
+    (1, 8, 2, 16, 130),
+    (1, 33, 1, 129, 17),
+    (3, 64, 5, 64, 64),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_split_volume_vs_oracle_and_exact(shape):
+    B, D, H, W1, W2 = shape
+    g = torch.Generator().manual_seed(31 * B + D + H + W1 + W2)
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    ref = coracle.corr_volume(f1.numpy(), f2.numpy())
+    with torch.no_grad():
+        sp = CorrBlock1D.corr(f1.to(DEV), f2.to(DEV)).cpu().numpy()
+        ex = CorrBlock1D.corr(f1.to(DEV), f2.to(DEV), exact_f32=True).cpu().numpy()
+    e_sp, e_ex = norm_err(sp, ref), norm_err(ex, ref)
+    l_sp, l_ex = rel_l2(sp, ref), rel_l2(ex, ref)
+    print(f"{shape}: split {e_sp:.2e}/{l_sp:.2e}  exact-f32 {e_ex:.2e}/{l_ex:.2e}")
+    assert e_sp <= 1e-4 and l_sp <= 1e-5
+    assert e_ex <= 1e-4 and l_ex <= 1e-5
+    assert e_sp <= max(2 * e_ex, 1e-6) and l_sp <= max(2 * l_ex, 1e-6)
+
+
+@pytest.mark.parametrize("levels", [2, 3, 4, 7], ids=lambda l: f"L{l}")
+def test_split_pyramid_levels_pool_bitexact(levels):
+    """Every stored level (eager build: all num_levels+1, incl. levels past the
+    5 the epilogue fuses) equals avg_pool2d of the level below bit for bit,
+    and level 0 is within the fp32 bound."""
+    B, D, H, W = 2, 64, 3, 240
+    g = torch.Generator().manual_seed(400 + levels)
+    f1 = torch.randn(B, D, H, W, generator=g)
+    f2 = torch.randn(B, D, H, W, generator=g)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=levels, radius=2, lazy_levels=False)
+        pyr = [t.reshape(t.shape[0], -1).cpu().numpy() for t in blk.corr_pyramid]
+    ref0 = coracle.corr_volume(f1.numpy(), f2.numpy()).reshape(B * H * W, W)
+    assert norm_err(pyr[0], ref0) <= 1e-4 and rel_l2(pyr[0], ref0) <= 1e-5
+    for l in range(1, levels + 1):
+        assert same(pyr[l], coracle.corr_pool(pyr[l - 1])), f"level {l}"
+
+
+def test_split_pair_layout_with_shadows_and_lookup():
+    """The product default (levels 0 + 2 stored, level-2 shadow) through the
+    split kernel: the pair lookup equals the per-level lookup on the
+    materialised pyramid bit for bit, and the oracle's sampler."""
+    B, D, H, W = 2, 256, 4, 240
+    g = torch.Generator().manual_seed(77)
+    f1 = torch.randn(B, D, H, W, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W, generator=g).to(DEV)
+    x = torch.arange(W).float().view(1, 1, 1, W) - torch.rand(B, 1, H, W, generator=g) * 64
+    coords = torch.cat([x, torch.zeros_like(x)], 1).to(DEV)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2)
+        assert blk.levels_stored == [0, 2] and 2 in blk._shadow
+        out = blk(coords)
+        ref = rcorr.lookup(blk.corr_pyramid, coords, 4, 4)
+        pyr = [t.reshape(t.shape[0], -1).cpu().numpy() for t in blk.corr_pyramid[:4]]
+    assert torch.equal(out, ref)
+    assert same(out.cpu().numpy(), coracle.corr_lookup(pyr, coords.cpu().numpy(), 4, 4))
+
+
+def test_split_special_values():
+    """Zeros, subnormals, large and tiny magnitudes stay within the fp32 bound
+    (the three pieces are exact for every finite fp32 below 3.39e38)."""
+    B, D, H, W = 1, 64, 2, 96
+    g = torch.Generator().manual_seed(5)
+    f1 = torch.randn(B, D, H, W, generator=g) * torch.logspace(-20, 20, W).view(1, 1, 1, W)
+    f2 = torch.randn(B, D, H, W, generator=g)
+    f1[0, :, 0, :8] = 0.0
+    f2[0, :3, 1, :] = 1e-40
+    ref = coracle.corr_volume(f1.numpy(), f2.numpy())
+    with torch.no_grad():
+        sp = CorrBlock1D.corr(f1.to(DEV), f2.to(DEV)).cpu().numpy()
+    # per w1 row (magnitudes differ by 40 decades across rows)
+    for w1 in range(W):
+        r, s = ref[:, :, w1], sp[:, :, w1]
+        if np.abs(r).max() > 0:
+            assert norm_err(s, r) <= 1e-5, w1
