@@ -36,6 +36,8 @@ from raft_stereo_amd import CorrBlock1D, coords_grid  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
+SPLIT_PRODUCTS = 6             # bf16 MFMAs per fp32 product in rc::build_split_kernel
 
 CONFIGS = {
     # name: (B per GPU, D, H1, W1, W2, levels, radius, iters, description)
@@ -342,17 +344,23 @@ def upsample_timing(cfg, device, reps=20):
             "shape": {"flow": [B, 1, H, W1], "mask": [B, 9 * f * f, H, W1], "factor": f}}
 
 
-def rcorr_pair(L, r, W2):
-    from raft_stereo_amd import corr as rcorr
-    return rcorr._pair_grads_ok(L, r, W2)
-
-
-def load_traffic(path):
+def load_pmc(path, config):
+    """profiles/pmc.json (tools/pmc_collect.py): per-kernel counters measured by
+    running THIS script for ``config`` under rocprofv3 --pmc; {} if absent."""
     try:
         with open(path) as fh:
-            return json.load(fh)
+            return json.load(fh).get(config, {})
     except (OSError, ValueError):
         return {}
+
+
+def pmc_entry(pmc, family):
+    """The one kernel of ``family`` (e.g. 'rc::lookup_pair_kernel') that the
+    PMC run of this config recorded: (exact name, entry), or (None, {}) when
+    there is none or more than one instance (then no counter is reported)."""
+    hits = [(k, v) for k, v in pmc.get("kernels", {}).items()
+            if k == family or k.startswith(family + "<")]
+    return hits[0] if len(hits) == 1 else (None, {})
 
 
 def main():
@@ -367,10 +375,15 @@ def main():
                     help="capture one step (build + lookups) in a HIP graph and replay it")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="also time the whole network this many steps (0 = skip)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
-    ap.add_argument("--mfma", default=os.path.join(ROOT, "profiles", "mfma.json"),
-                    help="PMC MFMA-busy fractions per kernel (written by tools/pmc_sq.py)")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc.json"),
+                    help="per-kernel PMC counters of this script's own kernels, per config "
+                         "(tools/pmc_collect.py)")
+    ap.add_argument("--pmc-calibrate", action="store_true",
+                    help="copy 1 GiB first (the FETCH_SIZE/WRITE_SIZE calibration dispatch of a "
+                         "rocprofv3 --pmc run, tools/pmc_collect.py)")
+    ap.add_argument("--exact-f32", action="store_true",
+                    help="fp32 builds on the exact fp32 MFMA kernel (RC_BUILD_EXACT_F32) instead of "
+                         "the split-bf16 default")
     ap.add_argument("--channels-last", action="store_true", default=None,
                     help="lookup output in NHWC memory order (CorrBlock1D(channels_last=True): "
                          "same shape and values); default for the bf16 config (kitti), whose "
@@ -399,6 +412,11 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local_dev)
     torch.cuda.set_device(device)
+    if args.pmc_calibrate:
+        big = torch.empty(1 << 28, device=device).fill_(1.0)
+        big.clone()
+        del big
+        torch.cuda.synchronize()
 
     cfg = CONFIGS[args.config]
     global_batch = args.config in GLOBAL_BATCH_CONFIGS
@@ -428,7 +446,7 @@ def main():
         if ev is not None:
             ev[0].record()
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
-                          low_latency=args.config in LOW_LATENCY_CONFIGS)
+                          low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
         if ev is not None:
             ev[1].record()
         for it in range(iters):
@@ -483,7 +501,7 @@ def main():
             for e0, e1 in be:
                 e0.record()
                 CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
-                          low_latency=args.config in LOW_LATENCY_CONFIGS)
+                            low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
                 e1.record()
             torch.cuda.synchronize()
             build_ms = sum(e0.elapsed_time(e1) for e0, e1 in be) / len(be)
@@ -493,7 +511,7 @@ def main():
         # GPU reaches them, so no event pair spans a host gap; median over 3
         # passes of all launches.
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
-                          low_latency=args.config in LOW_LATENCY_CONFIGS)
+                          low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
         per_launch = []
         for _ in range(3):
             le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
@@ -532,44 +550,56 @@ def main():
     lbytes = lookup_bytes(P, L, r, s_pyr=s_el)
     written = blk.levels_stored                      # levels the build wrote
     vbytes = volume_bytes(B, D, H, W1, W2, written, s_in=s_el, s_pyr=s_el)
-    traffic = load_traffic(args.traffic).get(args.config, {})
-    if bf16:   # HBM-bound in bf16: price the volume in bytes
-        vgbs = vbytes / (build_ms * 1e-3) / 1e9
-        roof_volume = {"bound": "hbm", "achieved": vgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": vgbs / HBM_PEAK_GBS, "traffic": traffic.get("build_bytes"),
-                       "algorithmic_bytes": vbytes, "flops": vflops,
-                       "kernel": ("rc::build_bf16_ring_kernel" if W2 > 64 else "rc::build_bf16_kernel"),
-                       "avg_launch_us": build_ms * 1e3,
-                       "levels_written": written, "shadow_levels": sorted(blk._shadow)}
+    pmc = load_pmc(args.pmc, args.config)
+    split = not bf16 and not args.exact_f32 and W1 % 4 == 0 and W2 % 4 == 0
+    vfamily = ("rc::build_bf16_ring_kernel" if bf16 and W2 > 64 else "rc::build_bf16_kernel" if bf16
+               else "rc::build_split_kernel" if split else "rc::build_f32_ring_kernel")
+    vname, vpmc = pmc_entry(pmc, vfamily)
+    vgbs = vbytes / (build_ms * 1e-3) / 1e9
+    roof_volume = {"bound": "hbm", "achieved": vgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": vgbs / HBM_PEAK_GBS, "traffic": vpmc.get("hbm_bytes"),
+                   "algorithmic_bytes": vbytes, "flops": vflops, "kernel": vname or vfamily,
+                   "avg_launch_us": build_ms * 1e3, "levels_written": written,
+                   "shadow_levels": sorted(blk._shadow)}
+    if bf16:
+        pass   # HBM-bound in bf16: priced in bytes
+    elif split:
+        # fp32 volume on bf16 MFMA (three-way split, six products per fp32
+        # product, csrc/volume_split.hip): its own roofline is HBM (8 TB/s for
+        # the bytes vs 2.5 PF for the executed bf16 FLOPs); also reported: the
+        # executed bf16 MFMA rate and the fp32-equivalent rate vs the fp32 peak
+        ex = SPLIT_PRODUCTS * vflops / (build_ms * 1e-3) / 1e12
+        roof_volume.update({
+            "mfma_bf16_executed_tflops": ex, "mfma_bf16_frac": ex / BF16_MFMA_PEAK_TFLOPS,
+            "fp32_equivalent_tflops": vflops / (build_ms * 1e-3) / 1e12,
+            "fp32_equivalent_frac_of_fp32_mfma_peak": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+            "arithmetic": "fp32 operands split exactly into 3 bf16 pieces; 6 bf16 MFMA products "
+                          "(v_mfma_f32_16x16x32_bf16, fp32 accumulate) per fp32 product"})
     else:
         roof_volume = {"bound": "mfma", "achieved": vflops / (build_ms * 1e-3) / 1e12,
                        "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                        "frac": vflops / (build_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                       "traffic": traffic.get("build_bytes"), "algorithmic_bytes": vbytes,
-                       "kernel": "rc::build_f32_ring_kernel<4,0>", "avg_launch_us": build_ms * 1e3,
+                       "traffic": vpmc.get("hbm_bytes"), "algorithmic_bytes": vbytes,
+                       "kernel": vname or vfamily, "avg_launch_us": build_ms * 1e3,
                        "levels_written": written, "shadow_levels": sorted(blk._shadow)}
+    if "mfma_util" in vpmc:
+        roof_volume["mfma_util_pmc"] = vpmc["mfma_util"]
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     pair = blk._chain and (L == 2 or (L == 4 and 2 in written))
-    lname = (f"rc::lookup_pair_kernel<{r},{L}>" if pair else
-             f"rc::lookup_chain_kernel<{r},{L},0>" if blk._chain
-             else f"rc::lookup_levelpar_kernel<{r},{'true' if bf16 else 'false'}>" if P < 65536 and L <= 4
-             else f"rc::lookup_kernel<{r},0,{'true' if bf16 else 'false'},true>")
-    ltraffic = traffic.get("lookup_pair_bytes" if pair else
-                           "lookup_chain_bytes" if blk._chain else "lookup_bytes")
+    lfamily = ("rc::lookup_pair_kernel" if pair else "rc::lookup_chain_kernel" if blk._chain
+               else "rc::lookup_levelpar_kernel" if P < 65536 and L <= 4 else "rc::lookup_kernel")
+    lname, lpmc = pmc_entry(pmc, lfamily)
+    ltraffic = lpmc.get("hbm_bytes")
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": lgbs / HBM_PEAK_GBS, "traffic": ltraffic,
-                   "algorithmic_bytes": lbytes, "kernel": lname,
+                   "algorithmic_bytes": lbytes, "kernel": lname or lfamily,
                    "avg_launch_us": lookup_launch_ms * 1e3}
     if ltraffic:   # the HBM bytes the kernel really moves (PMC), per second
         roof_lookup["traffic_gbs"] = ltraffic / (lookup_launch_ms * 1e-3) / 1e9
         roof_lookup["traffic_frac"] = roof_lookup["traffic_gbs"] / HBM_PEAK_GBS
-    mfma_pmc = load_traffic(args.mfma).get("kernels", {})
-
-    def pmc_util(prefix):
-        hit = [v for k, v in mfma_pmc.items() if prefix in k]
-        return hit[0]["mfma_util"] if hit else None
-    if not bf16:
-        roof_volume["mfma_util_pmc"] = pmc_util("build_f32_ring_kernel")
+        roof_lookup["traffic_over_algorithmic"] = ltraffic / lbytes
+    if pmc:
+        roof_lookup["pmc_source"] = f"{os.path.relpath(args.pmc, ROOT)} [{args.config}] {pmc.get('tag', '')}"
     dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
 
     result = {
@@ -608,13 +638,19 @@ def main():
     }
     if not args.no_backward and args.config == "sceneflow":
         result["backward"] = backward_timing(cfg, f1, f2, coords)
-        lbt = traffic.get("lookup_bwd_pair_bytes" if rcorr_pair(L, r, W2) else "lookup_bwd_bytes")
-        if lbt:   # PMC bytes the lookup backward really moves, per launch
-            rl = result["backward"]["roofline_lookup_bwd"]
-            rl["traffic"] = lbt
-            rl["traffic_gbs"] = lbt / (result["backward"]["lookup_bwd_us"] * 1e-6) / 1e9
+        rl = result["backward"]["roofline_lookup_bwd"]
+        bname, bpmc = pmc_entry(pmc, rl["kernel"].split("<")[0])
+        if bpmc.get("hbm_bytes"):   # PMC bytes the lookup backward really moves, per launch
+            rl["kernel"] = bname
+            rl["traffic"] = bpmc["hbm_bytes"]
+            rl["traffic_gbs"] = rl["traffic"] / (result["backward"]["lookup_bwd_us"] * 1e-6) / 1e9
             rl["traffic_frac"] = rl["traffic_gbs"] / HBM_PEAK_GBS
-        result["backward"]["roofline_volume_bwd"]["mfma_util_pmc"] = pmc_util("volume_bwd_kernel")
+            rl["traffic_over_algorithmic"] = rl["traffic"] / rl["algorithmic_bytes"]
+        rv = result["backward"]["roofline_volume_bwd"]
+        vbname, vbpmc = pmc_entry(pmc, "rc::volume_bwd_kernel")
+        if "mfma_util" in vbpmc:    # the exact instance the backward ran (one per config)
+            rv["kernel"] = vbname
+            rv["mfma_util_pmc"] = vbpmc["mfma_util"]
         result["upsample"] = upsample_timing(cfg, device)
     if args.e2e_steps > 0 and args.config == "sceneflow":
         result["e2e"] = e2e_pairs_per_s(cfg, device, args.e2e_steps, 1, world=world)

@@ -116,13 +116,13 @@ __device__ __forceinline__ void store_rows16(uint32_t st, int p, int cw, void *l
 __device__ __forceinline__ void store_rows16_any(uint32_t st, int p, int cw, void *lvl, long long ld,
                                                  bool bf16, long long rowbase, int w1_0, int col0,
                                                  int W1, int Wl, int lane, long long sh) {
-    // widest vector dividing the image width (col0 is a multiple of it) and
-    // the row stride
-    if (bf16 && ld % 8 == 0 && cw % 8 == 0)
+    // widest vector dividing the image width, the first column (so every
+    // vector is naturally aligned) and the row stride
+    if (bf16 && ld % 8 == 0 && cw % 8 == 0 && col0 % 8 == 0)
         store_rows16<8>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
-    else if (ld % 4 == 0 && cw % 4 == 0)
+    else if (ld % 4 == 0 && cw % 4 == 0 && col0 % 4 == 0)
         store_rows16<4>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
-    else if (ld % 2 == 0 && cw % 2 == 0)
+    else if (ld % 2 == 0 && cw % 2 == 0 && col0 % 2 == 0)
         store_rows16<2>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
     else
         store_rows16<1>(st, p, cw, lvl, ld, bf16, rowbase, w1_0, col0, W1, Wl, lane, sh);
@@ -137,9 +137,13 @@ __device__ __forceinline__ float pool2(float x, float y, bool bf) {
 // C[w1 = m0 + 16nb + (l&15)][w2 = n0 + 16ma + 4(l>>4) + r].  One fragment
 // column nb (16 w1 rows) at a time, every level: level l's image has rows
 // w1 - m0 - 16nb, columns (w2 - n0) >> l, pitch (WT >> l) + 4 floats.
+// w1_end: rows (w1) at or past it are not stored -- the image edge, or the
+// end of this wave's block when it covers fewer than 4 fragments of w1 inside
+// a tile (split kernel, volume_split.hip); -1 = a.W1.
 template <int FMA, int MODE, int NLM>
 __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const BuildArgs &a, int row,
-                                                 int m0, int n0, int lane0, uint32_t st0) {
+                                                 int m0, int n0, int lane0, uint32_t st0, int w1_end = -1) {
+    const int w1e = w1_end < 0 || w1_end > a.W1 ? a.W1 : w1_end;
     constexpr int WT = 16 * FMA;
     const bool bf = a.pyr_bf16 != 0;
     const long long rowbase = (long long)row * a.W1;
@@ -157,7 +161,7 @@ __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const Bui
         const int g = lane >> 4, i = lane & 15;
         auto flush = [&](int l) {
             const int cw = WT >> l;
-            store_rows16_any(st, cw + 4, cw, a.lvl[l], a.ld[l], bf, rowbase, m0 + 16 * nb, n0 >> l, a.W1,
+            store_rows16_any(st, cw + 4, cw, a.lvl[l], a.ld[l], bf, rowbase, m0 + 16 * nb, n0 >> l, w1e,
                              a.W2 >> l, lane, a.shadow[l]);
         };
         float v[FMA][4];

@@ -96,6 +96,8 @@ __device__ __forceinline__ SplitFrag sp_read(const char *base) {
 struct SpCtx {
     __amdgpu_buffer_rsrc_t r1, r2;
     int D, H, h, W1, W2, M0, N0, wave, lane, nst;
+    int tw1, tw2;      // tile extent (w) along w1 / w2: 16 x fragments, <= 128
+    int o1, o2;        // this wave's first column (w) inside the tile, w1 / w2
 };
 
 // DMA share of this wave per stage: rows 4w..4w+3 of both tiles, 2 rows
@@ -110,8 +112,9 @@ __device__ __forceinline__ void sp_issue(const SpCtx &c, char *smem, int st) {
         const int d = st * kSpBK + r0 + (c.lane >> 5);
         const int w = 4 * (c.lane & 31);
         const long long base = (long long)(d < c.D ? d : 0) * c.H + c.h;
-        const uint32_t offA = d < c.D ? (uint32_t)((base * c.W1 + c.M0 + w) * 4) : 0xFFFFFF00u;
-        const uint32_t offB = d < c.D ? (uint32_t)((base * c.W2 + c.N0 + w) * 4) : 0xFFFFFF00u;
+        // columns past the tile extent are not fetched (out-of-range offset)
+        const uint32_t offA = d < c.D && w < c.tw1 ? (uint32_t)((base * c.W1 + c.M0 + w) * 4) : 0xFFFFFF00u;
+        const uint32_t offB = d < c.D && w < c.tw2 ? (uint32_t)((base * c.W2 + c.N0 + w) * 4) : 0xFFFFFF00u;
         if constexpr (!(MODE & kModeNoLoads)) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r1, (lds_void *)(sA + (r0 >> 1) * kSpBlk), 16, (int)offA, 0, 0, 0);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r2, (lds_void *)(sB + (r0 >> 1) * kSpBlk), 16, (int)offB, 0, 0, 0);
@@ -124,7 +127,6 @@ __device__ __forceinline__ void sp_issue(const SpCtx &c, char *smem, int st) {
 // share and joins every barrier.
 template <int FA, int FB, int MODE, int NLM>
 __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, char *smem, int row) {
-    const int wm = c.wave & 1, wn = c.wave >> 1;         // w1 half (B), w2 half (A)
     const int lane = c.lane, i = lane & 15, g = lane >> 4;
     // lane (i, g) reads d rows 8(g & 1) .. +7 of stage (g >> 1) of the K step
     const int lrow = (g & 1) * 4 * kSpBlk;               // rows 8(g&1): 4 blocks in
@@ -153,8 +155,8 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
         }
         if constexpr (FA > 0 && !(MODE & kModeNoMath)) {
             const char *st = smem + ((2 * ks + (g >> 1)) % kSpSL) * kSpSlot + lrow;
-            const char *pb = st + 4 * (64 * wm + i);                     // F1 (B): this wave's w1
-            const char *pa = st + kSpOp + 4 * (64 * wn + i);             // F2 (A): this wave's w2
+            const char *pb = st + 4 * (c.o1 + i);                        // F1 (B): this wave's w1
+            const char *pa = st + kSpOp + 4 * (c.o2 + i);                // F2 (A): this wave's w2
             SplitFrag fb[FB];
 #pragma unroll
             for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE>(pb + 64 * n);
@@ -179,8 +181,8 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if constexpr (FA > 0)
-        epilogue_swapped<FA, MODE, NLM>(acc, a, row, c.M0 + 64 * wm, c.N0 + 64 * wn, lane,
-                                        lds_u32(smem + c.wave * kSpStb));
+        epilogue_swapped<FA, MODE, NLM>(acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
+                                        lds_u32(smem + c.wave * kSpStb), c.M0 + c.o1 + 16 * FB);
 }
 
 template <int FA, int MODE, int NLM>
@@ -192,27 +194,36 @@ __device__ __forceinline__ void split_fb(int fb, const SpCtx &c, const BuildArgs
 }
 
 template <int MODE, int NLM>
-__global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nwg_total) {
+__global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nwg_total, int tf1, int tf2,
+                                                             int tiles1, int tiles2) {
     __shared__ __attribute__((aligned(16))) char smem[kSpSL * kSpSlot];
     SpCtx c;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c.lane = threadIdx.x & 63;
-    const int T = a.tiles_m * a.tiles_n;
+    // tiles of tf1 x tf2 16-wide fragments (launcher: balanced over the row,
+    // at most 8 = 128 w); the four waves split them 2 x 2, ceil / floor
+    const int T = tiles1 * tiles2;
     const int wgid = xcd_remap(blockIdx.x, nwg_total);   // a row's tiles share an XCD (and its L2)
     const int row = wgid / T, tile = wgid - row * T;
-    const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+    const int tm = tile / tiles2, tn = tile - tm * tiles2;
     const int b = row / a.H;
     c.h = row - b * a.H;
     c.D = a.D; c.H = a.H; c.W1 = a.W1; c.W2 = a.W2;
-    c.M0 = tm * 128; c.N0 = tn * 128;
+    c.M0 = tm * 16 * tf1; c.N0 = tn * 16 * tf2;
+    c.tw1 = 16 * tf1; c.tw2 = 16 * tf2;
+    const int wm = c.wave & 1, wn = c.wave >> 1;
+    const int h1 = (tf1 + 1) >> 1, h2 = (tf2 + 1) >> 1;  // fragments of the first wave half
+    c.o1 = 16 * h1 * wm; c.o2 = 16 * h2 * wn;
     c.nst = 2 * ((a.D + 2 * kSpBK - 1) / (2 * kSpBK));   // whole K steps (d >= D reads zeros)
     const long long img1 = (long long)a.D * a.H * a.W1, img2 = (long long)a.D * a.H * a.W2;
     c.r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
     c.r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
-    // valid 16-wide fragments of this wave's 64 x 64 tile (wave-uniform)
-    const int cw2 = a.W2 - (c.N0 + 64 * (c.wave >> 1)), cw1 = a.W1 - (c.M0 + 64 * (c.wave & 1));
-    const int fa = cw2 <= 0 || cw1 <= 0 ? 0 : (cw2 >= 64 ? 4 : (cw2 + 15) >> 4);
-    const int fb = cw1 >= 64 ? 4 : (cw1 + 15) >> 4;
+    // valid 16-wide fragments of this wave's block (wave-uniform): its share
+    // of the tile, cut at the image edge
+    const int n1 = wm ? tf1 - h1 : h1, n2 = wn ? tf2 - h2 : h2;
+    const int cw1 = a.W1 - (c.M0 + c.o1), cw2 = a.W2 - (c.N0 + c.o2);
+    const int v1 = cw1 <= 0 ? 0 : min(n1, (cw1 + 15) >> 4), v2 = cw2 <= 0 ? 0 : min(n2, (cw2 + 15) >> 4);
+    const int fa = v1 == 0 ? 0 : v2, fb = v1;
     if (fa == 4) split_fb<4, MODE, NLM>(fb, c, a, smem, row);
     else if (fa == 3) split_fb<3, MODE, NLM>(fb, c, a, smem, row);
     else if (fa == 2) split_fb<2, MODE, NLM>(fb, c, a, smem, row);
@@ -238,28 +249,36 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
             if (!a.lvl[l]) return hipErrorNotSupported;
         a.nfused = rc::kSpMaxFused;
     }
-    const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
+    // balanced tiles: a row of nf fragments in ceil(nf / 8) tiles of equal
+    // size (W = 160: two of 5 fragments instead of 8 + 2; W = 240: 8 + 7)
+    auto tile_frags = [](int W) {
+        const int nf = (W + 15) / 16, nt = (nf + 7) / 8;
+        return (nf + nt - 1) / nt;
+    };
+    const int tf1 = tile_frags(a.W1), tf2 = tile_frags(a.W2);
+    const int tiles1 = ((a.W1 + 15) / 16 + tf1 - 1) / tf1, tiles2 = ((a.W2 + 15) / 16 + tf2 - 1) / tf2;
+    const long long nwg = (long long)a.B * a.H * tiles1 * tiles2;
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
 #ifdef RAFTCORR_DEV
     // dev-only ablations (timing only): RAFTCORR_SPLIT_MODE = kMode* flags
     // (1 no operand loads, 2 no epilogue stores, 4 no MFMAs; sums combine)
     switch (rc::dev_knob("RAFTCORR_SPLIT_MODE")) {
-        case 1: hipLaunchKernelGGL((rc::build_split_kernel<1, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
-        case 2: hipLaunchKernelGGL((rc::build_split_kernel<2, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
-        case 3: hipLaunchKernelGGL((rc::build_split_kernel<3, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
-        case 4: hipLaunchKernelGGL((rc::build_split_kernel<4, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
-        case 6: hipLaunchKernelGGL((rc::build_split_kernel<6, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
-        case 7: hipLaunchKernelGGL((rc::build_split_kernel<7, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg); return hipGetLastError();
+        case 1: hipLaunchKernelGGL((rc::build_split_kernel<1, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 2: hipLaunchKernelGGL((rc::build_split_kernel<2, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 3: hipLaunchKernelGGL((rc::build_split_kernel<3, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 4: hipLaunchKernelGGL((rc::build_split_kernel<4, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 6: hipLaunchKernelGGL((rc::build_split_kernel<6, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 7: hipLaunchKernelGGL((rc::build_split_kernel<7, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         default: break;
     }
 #endif
     // up to 3 fused levels (the pair layout: 0 and 2 stored) keeps the
     // epilogue's level pointers out of the scalar registers
     if (a.nfused <= 3)
-        hipLaunchKernelGGL((rc::build_split_kernel<0, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg);
+        hipLaunchKernelGGL((rc::build_split_kernel<0, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2);
     else
         hipLaunchKernelGGL((rc::build_split_kernel<0, rc::kSpMaxFused>), dim3((unsigned)nwg), dim3(256), 0, s, a,
-                           (int)nwg);
+                           (int)nwg, tf1, tf2, tiles1, tiles2);
     return hipGetLastError();
 }

@@ -31,6 +31,8 @@ SHAPES = [
     (1, 8, 2, 16, 130),
     (1, 33, 1, 129, 17),
     (3, 64, 5, 64, 64),
+    (1, 96, 3, 224, 224),       # tiles of 7 fragments: wave blocks of 4 + 3 inside the row
+    (1, 64, 2, 96, 176),        # 6 / 11 fragments: tiles of 6 and of 6 + 5
 ]
 
 
@@ -52,12 +54,14 @@ def test_split_volume_vs_oracle_and_exact(shape):
     assert e_sp <= max(2 * e_ex, 1e-6) and l_sp <= max(2 * l_ex, 1e-6)
 
 
-@pytest.mark.parametrize("levels", [2, 3, 4, 7], ids=lambda l: f"L{l}")
-def test_split_pyramid_levels_pool_bitexact(levels):
+@pytest.mark.parametrize("levels,W", [(2, 240), (3, 240), (4, 240), (7, 240), (4, 160), (4, 224),
+                                      (5, 208)], ids=lambda v: str(v))
+def test_split_pyramid_levels_pool_bitexact(levels, W):
     """Every stored level (eager build: all num_levels+1, incl. levels past the
     5 the epilogue fuses) equals avg_pool2d of the level below bit for bit,
-    and level 0 is within the fp32 bound."""
-    B, D, H, W = 2, 64, 3, 240
+    and level 0 is within the fp32 bound -- incl. widths whose balanced tiles
+    have fewer than 8 fragments (160: 5 + 5, 224: 7 + 7, 208: 7 + 6)."""
+    B, D, H = 2, 64, 3
     g = torch.Generator().manual_seed(400 + levels)
     f1 = torch.randn(B, D, H, W, generator=g)
     f2 = torch.randn(B, D, H, W, generator=g)
