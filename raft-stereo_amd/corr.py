@@ -433,16 +433,19 @@ def build_backward(fmap1, fmap2, grads):
 
 
 def default_shadow_levels(P, W2, num_levels, pyramid_dtype):
-    """Stored levels that get an RC_SHADOW copy by default (measured,
-    DESIGN.md §3.2e): level 2 of a 4-level pair layout always; level 0 only
-    when it is larger than the 256 MiB Infinity Cache -- a smaller level 0
-    mostly hits there across the loop's lookups, and a second copy would
-    double its cached footprint for a line saving it hardly needs (config 2:
-    l2 alone 1129 us per corr step, l0+l2 1140; config 3: l0+l2 6864, l2
-    alone 7013).  Each copy must fit the kernel's 4 GiB window."""
+    """Stored levels that get an RC_SHADOW copy by default (measured per
+    config with the corr step = build + 32 lookups, tools/shadow_probe.py,
+    profiles/r03/shadow_*.log): level 2 of a 4-level pair
+    layout always; level 0 only for a bf16 pyramid larger than the 256 MiB
+    Infinity Cache.  A bf16 span (40 B) then always fits one 128-B line, which
+    pays for the copy's writes (config 3, B=64: 6227 us per step with levels
+    0 + 2, 6288 with level 2 only); an fp32 level 0 saves too little per
+    lookup for its copy (config 4, 1.03 GB: 2376 us with levels 0 + 2, 2281
+    with level 2 only; config 2: 1072 vs 1056).  Each copy must fit the
+    kernel's 4 GiB window."""
     es = torch.tensor([], dtype=pyramid_dtype).element_size()
     lv = [2] if num_levels == 4 else []
-    if P * W2 * es > (256 << 20):
+    if pyramid_dtype == torch.bfloat16 and P * W2 * es > (256 << 20):
         lv.insert(0, 0)
     return tuple(l for l in lv if shadow_fits(P, W2 >> l, pyramid_dtype))
 

@@ -239,6 +239,9 @@ def main():
                                          n_downsample=3, hidden_dims=[96, 96, 96]),
         # BASELINE.json configs[0]: one 1x3x320x720 pair, 12 iterations, default args
         "e2e_config1": lambda: e2e_seeded_case(ref, "config1", 320, 720, 12, 101),
+        # BASELINE.json configs[2]'s image size: one 1x3x375x1242 pair, 32 iterations
+        # (the fp32 reference; the GPU test runs the bf16 corr path against it)
+        "e2e_config3": lambda: e2e_seeded_case(ref, "config3", 375, 1242, 32, 103),
     }
     for name, make in todo.items():
         if not only or name in only:

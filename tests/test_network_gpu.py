@@ -142,3 +142,28 @@ def test_config1_disparity_matches_reference(name, fuse):
     mae = float(np.abs(disp - z["disparity"]).mean())
     print(f"{name} [{fuse}]: final MAE {mae:.2e} px, max {np.abs(disp - z['disparity']).max():.2e}")
     assert mae <= MAE_PX, mae
+
+
+@pytest.mark.parametrize("name", [n for n in sorted(SEEDED) if SEEDED[n]["W"] == 1242])
+def test_config3_bf16_corr_path_disparity(name):
+    """BASELINE configs[2]'s image size (one 1x3x375x1242 pair, 32 iterations,
+    default args, seeded weights): the network with the bf16 corr path
+    (fmaps rounded to bf16, bf16 MFMA volume, bf16 pyramid -- what config 3
+    runs) against the fp32 reference's final disparity, north_star's 0.01 px
+    MAE bar (model.py:354-383 + the D8 tail; VERDICT r2 missing item 4)."""
+    import functools
+    from golden_util import image_digest, stereo_pair
+    case = SEEDED[name]
+    z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
+    img1, img2 = stereo_pair(1, case["H"], case["W"], case["seed"])
+    assert image_digest(img1, img2) == case["image_sha256"]
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs(**case["args"]),
+                       corr_block=functools.partial(CorrBlock1D, pyramid_dtype=torch.bfloat16))
+    model = model.eval().cuda()
+    with torch.no_grad():
+        flows = model(img1.cuda(), img2.cuda(), iters=case["iters"])
+    disp = flows[-1][:, 0].cpu().numpy()
+    mae = float(np.abs(disp - z["disparity"]).mean())
+    print(f"{name} bf16 corr path: final MAE {mae:.2e} px, max {np.abs(disp - z['disparity']).max():.2e}")
+    assert mae <= MAE_PX, mae
