@@ -133,8 +133,9 @@ def _instance_norm_rows(y, lo, hi, group, eps):
     mean = st[:N * C] / n
     var = (st[N * C:2 * N * C] / n - mean * mean).clamp_min(0)
     inv = torch.rsqrt(var + eps)
-    # fp32 out, as InstanceNorm under autocast
-    return (y.float() - mean.view(N, C, 1, 1).float()) * inv.view(N, C, 1, 1).float()
+    # fp32 out, as InstanceNorm under autocast (fp64 stays fp64)
+    dt = torch.promote_types(y.dtype, torch.float32)
+    return (y.to(dt) - mean.view(N, C, 1, 1).to(dt)) * inv.view(N, C, 1, 1).to(dt)
 
 
 class RowShardedStereo:
@@ -173,7 +174,7 @@ class RowShardedStereo:
     """
 
     def __init__(self, model, rank, world, halo=None, group=None, shard_encoders=True, enc_margin=48,
-                 per_stage=True):
+                 per_stage=True, encoder_halos=True):
         # one stage's cone needs 12 rows; a whole iteration's up to 20
         if halo is None:
             halo = 12 if per_stage else 24
@@ -187,6 +188,12 @@ class RowShardedStereo:
         self.model, self.rank, self.world, self.halo, self.group = model, rank, world, halo, group
         self.shard_encoders, self.enc_margin = shard_encoders, enc_margin
         self.per_stage = per_stage
+        # encoder_halos (default): each encoder module runs on this rank's own
+        # rows plus a halo refreshed from the neighbours right before it
+        # (_features_halo); False: a band of enc_margin extra rows recomputed
+        # locally (_features_rows)
+        self.encoder_halos = encoder_halos
+        self._fake_xchg = False     # tools/shard_probe.py: time one rank's compute alone
 
     # row geometry -----------------------------------------------------------
     def _ranges(self, H1):
@@ -295,6 +302,153 @@ class RowShardedStereo:
         inp = [[c[:, :, ext[l][0] - bl[l]:ext[l][1] - bl[l]] for c in inp_list[l]] for l in range(n)]
         return fmap1[:, :, sl], fmap2[:, :, sl], net, inp
 
+    # encoders with per-module halo exchange --------------------------------
+    def _halo(self, t, lo, hi, Hg, h):
+        """Slab of global rows [max(0, lo-h), min(Hg, hi+h)) from ``t`` (this
+        rank's own rows [lo, hi) of a level of height Hg): the h rows on
+        either side come from the neighbours' own boundary rows (every rank
+        owns >= h rows of every level).  Returns (slab, first global row)."""
+        g0, g1 = max(0, lo - h), min(Hg, hi + h)
+        if self.world == 1 or h == 0:
+            return t, lo
+        if self._fake_xchg:          # timing probe: same shapes, no communication
+            top = t.new_zeros(t.shape[:2] + (lo - g0,) + t.shape[3:])
+            bot = t.new_zeros(t.shape[:2] + (g1 - hi,) + t.shape[3:])
+            return torch.cat([top, t, bot], 2), g0
+        dev = t.device
+        staged = _host_staged(t, self.group)
+        src = t.cpu() if staged else t
+        ops, top, bot = [], None, None
+        if lo > 0:
+            top = torch.empty_like(src[:, :, :lo - g0]).contiguous()
+            ops += [dist.P2POp(dist.irecv, top, self.rank - 1, group=self.group),
+                    dist.P2POp(dist.isend, src[:, :, :min(h, hi - lo)].contiguous(), self.rank - 1,
+                               group=self.group)]
+        if hi < Hg:
+            bot = torch.empty_like(src[:, :, :g1 - hi]).contiguous()
+            ops += [dist.P2POp(dist.irecv, bot, self.rank + 1, group=self.group),
+                    dist.P2POp(dist.isend, src[:, :, max(0, hi - lo - h):].contiguous(), self.rank + 1,
+                               group=self.group)]
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+        seq = ([top.to(dev) if staged else top] if top is not None else []) + [t]
+        seq += [bot.to(dev) if staged else bot] if bot is not None else []
+        return torch.cat(seq, 2), g0
+
+    @staticmethod
+    def _crop(y, lo, hi, g0, stride):
+        """Own rows of a module output computed on a slab starting at global
+        row g0 (even when stride == 2): returns (rows, lo', hi')."""
+        if stride == 1:
+            return y[:, :, lo - g0:hi - g0], lo, hi
+        lo2, hi2 = lo // 2, (hi + 1) // 2
+        return y[:, :, lo2 - g0 // 2:hi2 - g0 // 2], lo2, hi2
+
+    def _run(self, mod, t, lo, hi, Hg, need, stride=1, slab=None):
+        """Apply ``mod`` (receptive field +-need rows at its input, ``stride``
+        1 or 2, padding preserving the grid) to own rows [lo, hi) of a level of
+        height Hg; ``slab`` = an already exchanged (tensor, g0).  Returns the
+        output's own rows and (lo, hi, Hg) at its level."""
+        if stride == 2 and need % 2:
+            need += 1                # the slab must start on an even row
+        x, g0 = slab if slab is not None else self._halo(t, lo, hi, Hg, need)
+        y, lo2, hi2 = self._crop(mod(x), lo, hi, g0, stride)
+        return y, lo2, hi2, (Hg if stride == 1 else (Hg + 1) // 2)
+
+    def _features_halo(self, image1, image2, r0, r1):
+        """RAFTStereo.features (model.py:339-364) on this rank's OWN rows:
+        every encoder module (stem, each ResidualBlock of layer1-5, each head,
+        conv2, the context convs) runs on its own rows plus the halo its
+        receptive field needs at that resolution (3x3 convs: 1 row each; a
+        residual block 2; a stride-2 block 4 at its input), refreshed from the
+        two neighbours right before it (_halo, point-to-point) -- SURVEY.md §8e
+        item 2, without recomputing a margin.  The image itself is replicated,
+        so the stem reads its rows directly.  conv2's InstanceNorms use
+        image-wide statistics (one all-reduce each, _instance_norm_rows).
+        Returns own rows of fmap1, fmap2 (1/f res) and of every level's net /
+        inp tensors, with (lo, hi, H) per level."""
+        m, a = self.model, self.model.args
+        if m.training:
+            raise RuntimeError("RowShardedStereo: encoder row sharding needs eval mode "
+                               "(BatchNorm running statistics)")
+        cn = m.cnet
+        f = 2 ** a.n_downsample
+        H = image1.shape[2]
+        lo, hi = min(H, r0 * f), min(H, r1 * f)
+        img = torch.cat(((2 * (image1 / 255.0) - 1.0), (2 * (image2 / 255.0) - 1.0)), 0)
+        n = a.n_gru_layers
+        B = image1.shape[0]
+        with m._autocast():
+            # stem: conv1 7x7 (+ BatchNorm, ReLU); the image is on every rank
+            s0 = cn.conv1.stride[0]
+            need = 4 if s0 == 2 else 3
+            g0 = max(0, lo - need)
+            stem = lambda z: cn.relu1(cn.norm1(cn.conv1(z)))  # noqa: E731
+            x, lo, hi, Hg = self._run(stem, None, lo, hi, H, need, s0,
+                                      slab=(img[:, :, g0:min(H, hi + need)].contiguous(), g0))
+            for layer in (cn.layer1, cn.layer2, cn.layer3):
+                for blk in layer:
+                    st = blk.conv1.stride[0]
+                    x, lo, hi, Hg = self._run(blk, x, lo, hi, Hg, 4 if st == 2 else 2, st)
+            assert (lo, hi) == (r0, r1), (lo, hi, r0, r1)
+            H1, levels = Hg, [(lo, hi, Hg)]
+            xs = self._halo(x, lo, hi, Hg, 4)              # heads08 and conv2 read x
+            outs = [[self._run(hd, None, lo, hi, Hg, 3, 1, slab=(xs[0][:B], xs[1]))[0]
+                     for hd in cn.outputs08]]
+            # conv2 (ResidualBlock with InstanceNorm + 3x3 conv), both images
+            blk2, conv = m.conv2[0], m.conv2[1]
+            xx, gx = xs
+            ol, oh = lo - gx, hi - gx                      # own rows, slab-local
+            eps = blk2.norm1.eps
+            y = blk2.relu(_instance_norm_rows(blk2.conv1(xx), ol, oh, self.group, eps))
+            y = blk2.relu(_instance_norm_rows(blk2.conv2(y), ol, oh, self.group, eps))
+            fm = conv(xx + y)[:, :, ol:oh]
+            fmap1, fmap2 = fm[:B], fm[B:]
+            if n >= 2:
+                y = x[:B]
+                for i, blk in enumerate(cn.layer4):
+                    st = blk.conv1.stride[0]
+                    y, lo, hi, Hg = self._run(blk, y, lo, hi, Hg, 4 if st == 2 else 2, st)
+                levels.append((lo, hi, Hg))
+                ys = self._halo(y, lo, hi, Hg, 4)
+                outs.append([self._run(hd, None, lo, hi, Hg, 3, 1, slab=ys)[0] for hd in cn.outputs16])
+                if n >= 3:
+                    for i, blk in enumerate(cn.layer5):
+                        st = blk.conv1.stride[0]
+                        y, lo, hi, Hg = self._run(blk, y, lo, hi, Hg, 4 if st == 2 else 2, st,
+                                                  slab=ys if i == 0 else None)
+                    levels.append((lo, hi, Hg))
+                    zs = self._halo(y, lo, hi, Hg, 2)
+                    outs.append([self._run(hd, None, lo, hi, Hg, 1, 1, slab=zs)[0] for hd in cn.outputs32])
+            net = [torch.tanh(o[0]) for o in outs]
+            inp = []
+            for l, (o, c) in enumerate(zip(outs, m.context_zqr_convs)):
+                ql, qh, qH = levels[l]
+                z = self._run(c, torch.relu(o[1]), ql, qh, qH, 1, 1)[0]
+                inp.append(list(z.split(dim=1, split_size=c.out_channels // 3)))
+        return fmap1, fmap2, net, inp, levels, H1
+
+    def _gru_slabs(self, fmap1, fmap2, net, inp, levels):
+        """Own rows -> the GRU slabs [e0, e1) (halo >> l at level l), one
+        exchange per level (all of that level's tensors side by side)."""
+        out_f, out_n, out_i = None, [], []
+        for l, (lo, hi, Hg) in enumerate(levels):
+            parts = ([fmap1, fmap2] if l == 0 else []) + [net[l]] + inp[l]
+            sizes = [p.shape[1] for p in parts]
+            dt = parts[0].dtype
+            for p in parts[1:]:
+                dt = torch.promote_types(dt, p.dtype)
+            cat = torch.cat([p.to(dt) for p in parts], 1)
+            slab, _ = self._halo(cat, lo, hi, Hg, self.halo >> l)
+            pieces = list(slab.split(sizes, 1))
+            pieces = [pc.to(p.dtype) for pc, p in zip(pieces, parts)]
+            if l == 0:
+                out_f = (pieces[0].contiguous(), pieces[1].contiguous())
+                pieces = pieces[2:]
+            out_n.append(pieces[0])
+            out_i.append(pieces[1:])
+        return out_f[0], out_f[1], out_n, out_i
+
     # forward ----------------------------------------------------------------
     def forward(self, image1, image2, iters=12):
         m, a = self.model, self.model.args
@@ -305,7 +459,12 @@ class RowShardedStereo:
             glob = self._heights(image1.shape[2], a.n_downsample, nl)
             H1 = glob[0]
             r0, r1, e0, e1 = self._ranges(H1)
-            fmap1, fmap2, net, inp = self._features_rows(image1, image2, e0, e1, r0, r1)
+            if self.encoder_halos:
+                f1o, f2o, no, io, lv, _ = self._features_halo(image1, image2, r0, r1)
+                assert [h for _, _, h in lv] == glob, (lv, glob)
+                fmap1, fmap2, net, inp = self._gru_slabs(f1o, f2o, no, io, lv)
+            else:
+                fmap1, fmap2, net, inp = self._features_rows(image1, image2, e0, e1, r0, r1)
         else:
             fmap1, fmap2, net_full, inp_full = m.features(image1, image2)
             H1 = fmap1.shape[2]

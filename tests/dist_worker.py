@@ -140,6 +140,52 @@ def run_features(rank, world, port, q, halo=24, H=800, W=64):
         dist.destroy_process_group()
 
 
+def run_features_halo(rank, world, port, q, halo=12, H=800, W=64, n_gru_layers=3, n_downsample=2,
+                      f64=False):
+    """Encoders on this rank's OWN rows with per-module halo exchange
+    (RowShardedStereo._features_halo + _gru_slabs) vs the full-image encoders
+    sliced to the rank's GRU slab [e0, e1): max |diff| over fmap1, fmap2 and
+    every level's net / inp tensors, and the own 1/f row range."""
+    import torch
+    import torch.distributed as dist
+    import pkgload
+    pkgload.load()
+    from raft_stereo_amd.network import RAFTStereo, StereoArgs
+    from raft_stereo_amd.shard import RowShardedStereo
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    try:
+        g = torch.Generator().manual_seed(11)
+        img1 = torch.rand(1, 3, H, W, generator=g) * 255
+        img2 = torch.roll(img1, -3, dims=-1)
+        torch.manual_seed(0)
+        net = RAFTStereo(StereoArgs(n_gru_layers=n_gru_layers, n_downsample=n_downsample)).eval()
+        if f64:       # exactness of the halo bookkeeping, free of fp32 conv-algorithm rounding
+            net, img1, img2 = net.double(), img1.double(), img2.double()
+        rs = RowShardedStereo(net, rank, world, halo=halo)
+        with torch.no_grad():
+            f1, f2, nf, inf = net.features(img1, img2)
+            H1 = f1.shape[2]
+            r0, r1, e0, e1 = rs._ranges(H1)
+            o1, o2, no, io, lv, _ = rs._features_halo(img1, img2, r0, r1)
+            s1, s2, ns, ins = rs._gru_slabs(o1, o2, no, io, lv)
+            d = max((s1 - f1[:, :, e0:e1]).abs().max().item(), (s2 - f2[:, :, e0:e1]).abs().max().item())
+            for l in range(len(nf)):
+                lo, hi = rs._lvl(e0, e1, l)
+                assert ns[l].shape[2] == hi - lo, (l, ns[l].shape, lo, hi)
+                d = max(d, (ns[l] - nf[l][:, :, lo:hi]).abs().max().item())
+                for a, b in zip(ins[l], inf[l]):
+                    d = max(d, (a - b[:, :, lo:hi]).abs().max().item())
+        q.put((rank, d, (H1, (r0, r1))))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
+
+
 def gpu_model():
     """The default network with the HIP corr block, on cuda:0, seeded weights."""
     import torch

@@ -114,3 +114,25 @@ def test_gloo_row_sharded_encoders_match_full(world):
         assert res[r][0] < 2e-5, (r, res[r][0])
     # the bands are proper sub-ranges: encoders really ran on part of the image
     assert any(b != (0, H1) for _, (_, b) in ((r, res[r][1]) for r in range(world)))
+
+
+@pytest.mark.parametrize("world,H,layers,down,f64", [(2, 800, 3, 2, True), (3, 375, 3, 2, True),
+                                                     (2, 640, 2, 3, True), (3, 800, 3, 2, False)])
+def test_gloo_encoder_halo_exchange_matches_full(world, H, layers, down, f64):
+    """the encoders run on each rank's OWN rows, every
+    module's halo (1-4 rows at its own resolution) refreshed from the two
+    neighbours right before it (point-to-point, no recomputed margin), and the
+    GRU slabs then assembled by one more exchange per level: equal to the
+    full-image features on the rank's slab (model.py:136-161, :345).  In
+    float64 to 1e-12 (the only differences are the summation order of
+    conv2's InstanceNorm statistics); in fp32 to 5e-5 absolute (measured
+    2.3e-5 on the 1/16-res heads: CPU convolutions pick other algorithms for
+    other input heights, 1e-6 relative to values up to 20)."""
+    res = _spawn(dist_worker.run_features_halo, world, 12, H, 64, layers, down, f64)
+    for r in range(world):
+        assert res[r][0] < (1e-12 if f64 else 5e-5), (r, res[r][0])
+    # own rows really partition the 1/f grid (no rank computed the whole image)
+    owns = sorted(res[r][1][1] for r in range(world))
+    H1 = res[0][1][0]
+    assert owns[0][0] == 0 and owns[-1][1] == H1
+    assert all(a[1] == b[0] for a, b in zip(owns, owns[1:]))

@@ -9,9 +9,14 @@ keeping a +-halo slab, and either runs the encoders (cnet + conv2 + context
 convs, model.py:359-365) replicated on the full image or (default) on a band
 of image rows around its slab (``shard_encoders``).  Timed here:
   E    = RAFTStereo.features on the full image (the replicated encoders);
-  Es(N)= the encoders on the widest rank's band (a middle rank: slab +
-         2 x enc_margin rows; the one InstanceNorm all-reduce of each of
-         conv2's two norms is not included -- a few KB);
+  Es(N)= the encoders of a middle rank with per-module halo exchange
+         (RowShardedStereo._features_halo + _gru_slabs, the default): its own
+         rows plus 1-4 halo rows per module; timed in one process with the
+         exchanges replaced by zero rows of the same shapes (_fake_xchg), so
+         the messages themselves (tens of KB to a few MB per module, one xGMI
+         hop) and the two InstanceNorm all-reduces are not included;
+  Eb(N)= the same rank's encoders on a band of +-enc_margin recomputed rows
+         (RowShardedStereo._features_rows, encoder_halos=False);
   C(n) = the corr build of an n-row slab;
   U(n) = one iteration on an n-row slab: lookup + update block (with the
          slab-local interp of RowShardedStereo._gru), n = H1/N + 2*halo;
@@ -95,22 +100,31 @@ def main():
                                           align_corners=True), True, True, True)
             U = timed(one_iter)
             T = E + C + a.iters * U
-            if N > 1:   # a middle rank's band (single process: no all-reduce)
+            if N > 1:   # a middle rank (single process: no messages, no all-reduce)
                 rm = RowShardedStereo(model, N // 2, N, halo=a.halo)
+                rm._fake_xchg = True
                 q0, q1, x0, x1 = rm._ranges(H1)
-                Es = timed(lambda: rm._features_rows(img1, img2, x0, x1, q0, q1))
+
+                def halo_features():
+                    o = rm._features_halo(img1, img2, q0, q1)
+                    return rm._gru_slabs(o[0], o[1], o[2], o[3], o[4])
+                Es = timed(halo_features)
+                Eb = timed(lambda: rm._features_rows(img1, img2, x0, x1, q0, q1))
                 band = min(H1, x1 + rm.enc_margin) - max(0, x0 - rm.enc_margin)
+                own = q1 - q0
             else:
-                Es, band = E, H1
-            out[N] = {"slab_rows": n, "C_build_ms": C * 1e3, "U_iter_ms": U * 1e3,
-                      "T_ms": T * 1e3, "Es_band_ms": Es * 1e3, "band_rows": band,
-                      "Ts_sharded_ms": (Es + C + a.iters * U) * 1e3}
+                Es, Eb, band, own = E, E, H1, H1
+            out[N] = {"slab_rows": n, "own_rows": own, "C_build_ms": C * 1e3, "U_iter_ms": U * 1e3,
+                      "T_ms": T * 1e3, "Es_halo_ms": Es * 1e3, "Eb_band_ms": Eb * 1e3,
+                      "band_rows": band, "Ts_sharded_ms": (Es + C + a.iters * U) * 1e3,
+                      "Tb_band_ms": (Eb + C + a.iters * U) * 1e3}
             print(f"N={N}: {json.dumps(out[N])}", flush=True)   # progress (long run)
         T1 = out[1]["T_ms"]
         for N in out:
             out[N]["speedup"] = T1 / out[N]["T_ms"]
             out[N]["encoder_share"] = res["E_encoders_ms"] / out[N]["T_ms"]
             out[N]["speedup_sharded"] = T1 / out[N]["Ts_sharded_ms"]
+            out[N]["speedup_band"] = T1 / out[N]["Tb_band_ms"]
         res["per_N"] = out
         res["amdahl_cap"] = T1 / res["E_encoders_ms"]
     print(json.dumps(res, indent=1))
