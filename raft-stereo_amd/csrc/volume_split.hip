@@ -231,7 +231,272 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nw
     else split_body<0, 1, MODE, NLM>(c, a, smem, row);
 }
 
+#ifdef RAFTCORR_DEV
+// ====== warp-specialised persistent split kernel: every element split once ======
+// DEV LIBRARY ONLY (RAFTCORR_SPLIT_KERNEL=3): measured and not kept --
+// config 2: 383 us against 283 for build_split_kernel.
+//
+// The kernel above splits every fragment in the registers of each wave that
+// reads it, i.e. twice (each operand tile is shared by two of the four
+// waves), and its VALU -- not the matrix pipe -- sets its pace (DESIGN.md
+// §3.1c).  Here a workgroup of 8 waves owns a CU: waves 0-3 compute (the same
+// 2 x 2 wave tiles, swapped operands, epilogue_swapped), waves 4-7 load:
+//   raw ring   2 slots x [2 operands][32 d][128 w] fp32 (64 KB), filled by
+//              LDS-DMA (buffer_load_dwordx4 ... lds, 1 KB per instruction);
+//   plane ring 2 slots x [2 operands][3 pieces][128 rows][32 d] bf16 (96 KB),
+//              written by the loaders: each splits its 4 (operand, w, 8-d)
+//              items of a K step once (raw via ds_read2_b32, planes via
+//              ds_write_b128 at the conflict-free chunk swizzle of v1);
+// 160 KB in all.  One s_barrier per K step g: after it the compute waves
+// multiply planes(g) while the loaders issue the DMA of raw(g+2) into the raw
+// slot of raw(g), split raw(g+1) into the other plane slot and wait for
+// raw(g+2).  Loaders never store and compute waves never load from global
+// memory, so neither role's vmcnt mixes loads with stores.  At a tile's last
+// K step a second barrier lets the compute waves stage the epilogue in the
+// plane slot they just finished; they arrive at the next K step's barrier
+// after it, so the loaders cannot overwrite the staging.  Persistent walk
+// over the tiles in XCD-contiguous runs (as build_bf16_ring_kernel).
+constexpr int kWsRaw = 32 * 128 * 4;                 // one operand of a raw K step
+constexpr int kWsRawSlot = 2 * kWsRaw;               // 32 KB
+constexpr int kWsPlane = 128 * 64;                   // [128 rows][32 d] bf16
+constexpr int kWsPlaneSlot = 6 * kWsPlane;           // 48 KB
+constexpr int kWsLds = 2 * kWsRawSlot + 2 * kWsPlaneSlot;
+static_assert(kWsLds <= 163840, "LDS");
+static_assert(4 * kSpStb <= kWsPlaneSlot, "epilogue staging fits a plane slot");
+
+__device__ __forceinline__ uint32_t ws_swz(int r, int c) { return (uint32_t)(r * 64 + 16 * (c ^ (-(r >> 2) & 3))); }
+
+struct WsTile {
+    int row, b, h, M0, N0;
+};
+
+__device__ __forceinline__ void ws_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// One K step of one compute wave: FA x FB fragments of plane slot ps.
+template <int FA, int FB, int MODE>
+__device__ __forceinline__ void ws_mma(f32x4 (&acc)[FA > 0 ? FA : 1][4], const char *ps, int o1, int o2,
+                                       uint32_t loff) {
+    if constexpr (FA > 0 && !(MODE & kModeNoMath)) {
+        const char *pb = ps + o1 * 64 + loff;                   // F1 planes (B): this wave's w1
+        const char *pa = ps + 3 * kWsPlane + o2 * 64 + loff;    // F2 planes (A): this wave's w2
+        bf16x8 bh[FB], bm[FB], bl[FB], ah[FA], am[FA], al[FA];
+#pragma unroll
+        for (int n = 0; n < FB; ++n) {
+            bh[n] = *reinterpret_cast<const bf16x8 *>(pb + 1024 * n);
+            bm[n] = *reinterpret_cast<const bf16x8 *>(pb + kWsPlane + 1024 * n);
+            bl[n] = *reinterpret_cast<const bf16x8 *>(pb + 2 * kWsPlane + 1024 * n);
+        }
+#pragma unroll
+        for (int m = 0; m < FA; ++m) {
+            ah[m] = *reinterpret_cast<const bf16x8 *>(pa + 1024 * m);
+            am[m] = *reinterpret_cast<const bf16x8 *>(pa + kWsPlane + 1024 * m);
+            al[m] = *reinterpret_cast<const bf16x8 *>(pa + 2 * kWsPlane + 1024 * m);
+        }
+#pragma unroll
+        for (int m = 0; m < FA; ++m)
+#pragma unroll
+            for (int n = 0; n < FB; ++n) {
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[m], bm[n], acc[m][n], 0, 0, 0);
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], bl[n], acc[m][n], 0, 0, 0);
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[m], bh[n], acc[m][n], 0, 0, 0);
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], bm[n], acc[m][n], 0, 0, 0);
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[m], bh[n], acc[m][n], 0, 0, 0);
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], bh[n], acc[m][n], 0, 0, 0);
+            }
+    }
+}
+
+// A compute wave's whole tile: nks K steps (one barrier each, global step g0
+// onwards), then the tile-end barrier and the epilogue.
+template <int FA, int FB, int MODE, int NLM>
+__device__ __forceinline__ void ws_tile(const BuildArgs &a, char *smem, const WsTile &t, int g0, int nks, int o1,
+                                        int o2, int lane) {
+    f32x4 acc[FA > 0 ? FA : 1][4];
+#pragma unroll
+    for (int x0 = 0; x0 < (FA > 0 ? FA : 1); ++x0)
+#pragma unroll
+        for (int y0 = 0; y0 < 4; ++y0) acc[x0][y0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int i = lane & 15, g = lane >> 4;
+    const uint32_t loff = (uint32_t)(i * 64 + 16 * (g ^ (-(i >> 2) & 3)));
+    for (int k = 0; k < nks; ++k) {
+        ws_barrier();                                             // B(g): planes(g) written
+        ws_mma<FA, FB, MODE>(acc, smem + 2 * kWsRawSlot + ((g0 + k) & 1) * kWsPlaneSlot, o1, o2, loff);
+    }
+    ws_barrier();                                                 // E: every wave done with planes(g)
+    if constexpr (FA > 0) {
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        char *st = smem + 2 * kWsRawSlot + ((g0 + nks - 1) & 1) * kWsPlaneSlot + wave * kSpStb;
+        epilogue_swapped<FA, MODE, NLM>(acc, a, t.row, t.M0 + o1, t.N0 + o2, lane, lds_u32(st),
+                                        t.M0 + o1 + 16 * FB);
+    }
+}
+
+template <int FA, int MODE, int NLM>
+__device__ __forceinline__ void ws_tile_fb(int fb, const BuildArgs &a, char *smem, const WsTile &t, int g0,
+                                           int nks, int o1, int o2, int lane) {
+    if (fb >= 4) ws_tile<FA, 4, MODE, NLM>(a, smem, t, g0, nks, o1, o2, lane);
+    else if (fb == 3) ws_tile<FA, 3, MODE, NLM>(a, smem, t, g0, nks, o1, o2, lane);
+    else if (fb == 2) ws_tile<FA, 2, MODE, NLM>(a, smem, t, g0, nks, o1, o2, lane);
+    else ws_tile<FA, 1, MODE, NLM>(a, smem, t, g0, nks, o1, o2, lane);
+}
+
+template <int MODE, int NLM>
+__global__ __launch_bounds__(512, 1) void build_split_ws_kernel(BuildArgs a, int ntiles, int tf1, int tf2,
+                                                                  int tiles1, int tiles2) {
+    __shared__ __attribute__((aligned(16))) char smem[kWsLds];
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int D = a.D, H = a.H, W1 = a.W1, W2 = a.W2;
+    const int T = tiles1 * tiles2;
+    // persistent walk: the tiles are cut into 8 contiguous runs, one per XCD
+    // (workgroup v runs on XCD v % 8), taken round-robin by its workgroups
+    const int nwg = gridDim.x, v = blockIdx.x;
+    const int xcd = v & 7, lw = v >> 3;
+    const int gx = (nwg - xcd + 7) >> 3;
+    const int before = xcd * (nwg >> 3) + min(xcd, nwg & 7);
+    const int t0 = (int)((long long)ntiles * before / nwg);
+    const int t1 = (int)((long long)ntiles * (before + gx) / nwg);
+    auto tile_at = [&](int k) {
+        WsTile t;
+        const int id = t0 + lw + k * gx;
+        t.row = id / T;
+        const int tl = id - t.row * T, tm = tl / tiles2, tn = tl - tm * tiles2;
+        t.b = t.row / H;
+        t.h = t.row - t.b * H;
+        t.M0 = tm * 16 * tf1;
+        t.N0 = tn * 16 * tf2;
+        return t;
+    };
+    const int nmine = t0 + lw < t1 ? (t1 - t0 - lw + gx - 1) / gx : 0;
+    if (nmine == 0) return;                                       // workgroup-uniform
+    const int nks = (D + 31) / 32;
+    const int total = nmine * nks;
+    const int tw1 = 16 * tf1, tw2 = 16 * tf2;
+
+    if (wave >= 4) {
+        // ------------------------------ loaders ------------------------------
+        const int lt = threadIdx.x - 256, lw4 = wave - 4;
+        const int r = lt & 127, cb = lt >> 7;
+        const long long img1 = (long long)D * H * W1, img2 = (long long)D * H * W2;
+        // DMA of global K step gs (tile gs / nks, step gs % nks) into raw slot gs & 1
+        auto dma = [&](int gs) {
+            const WsTile t = tile_at(gs / nks);
+            const int s = gs - (gs / nks) * nks;
+            const auto r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + t.b * img1, clamp_bytes(img1 * 4));
+            const auto r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + t.b * img2, clamp_bytes(img2 * 4));
+            char *slot = smem + (gs & 1) * kWsRawSlot;
+            const int w = 4 * (lane & 31);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int ins = 8 * lw4 + k;                      // 0..15 F1 rows, 16..31 F2 rows
+                const int o = ins >> 4, rp = ins & 15;            // operand, row pair
+                const int d = 32 * s + 2 * rp + (lane >> 5);
+                const int Wo = o ? W2 : W1, org = o ? t.N0 : t.M0, tw = o ? tw2 : tw1;
+                const bool ok = d < D && w < tw && org + w < Wo;
+                const uint32_t off = ok ? (uint32_t)((((long long)d * H + t.h) * Wo + org + w) * 4) : 0xFFFFFF00u;
+                if constexpr (!(MODE & kModeNoLoads))
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(o ? r2 : r1, (lds_void *)(slot + o * kWsRaw + rp * 1024),
+                                                             16, (int)off, 0, 0, 0);
+            }
+        };
+        // L2 touch of K step gs: one dword per 128-B line of its 32 KB (one
+        // load per loader lane), so the DMA two steps later hits L2; the value
+        // is never used and the load stays outside every vmcnt wait but the
+        // last (it is issued after the DMA, and loads complete in order)
+        auto touch = [&](int gs) {
+            if constexpr (!(MODE & kModeNoLoads) && !(MODE & 64)) {
+                const WsTile t = tile_at(gs / nks);
+                const int s = gs - (gs / nks) * nks;
+                const int o = lt >> 7, q = lt & 127;              // 128 lines per operand
+                const int d = 32 * s + (q >> 2), w = 32 * (q & 3);
+                const int Wo = o ? W2 : W1, org = o ? t.N0 : t.M0, tw = o ? tw2 : tw1;
+                const long long img = o ? img2 : img1;
+                const auto rr = make_rsrc(reinterpret_cast<const float *>(o ? a.f2 : a.f1) + t.b * img,
+                                          clamp_bytes(img * 4));
+                const bool ok = d < D && w < tw && org + w < Wo;
+                const uint32_t off = ok ? (uint32_t)((((long long)d * H + t.h) * Wo + org + w) * 4) : 0xFFFFFF00u;
+                const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)off, 0, 0));
+                asm volatile("" ::"v"(v));
+            }
+        };
+        // split raw K step gs into plane slot gs & 1
+        auto split = [&](int gs) {
+            const char *raw = smem + (gs & 1) * kWsRawSlot;
+            char *pl = smem + 2 * kWsRawSlot + (gs & 1) * kWsPlaneSlot;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int o = j >> 1, c = cb + 2 * (j & 1);
+                float x[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    x[q] = *reinterpret_cast<const float *>(raw + o * kWsRaw + (8 * c + q) * 512 + 4 * r);
+                const SplitFrag f = sp_split(x);
+                char *dst = pl + o * 3 * kWsPlane + ws_swz(r, c);
+                *reinterpret_cast<bf16x8 *>(dst) = f.h;
+                *reinterpret_cast<bf16x8 *>(dst + kWsPlane) = f.m;
+                *reinterpret_cast<bf16x8 *>(dst + 2 * kWsPlane) = f.l;
+            }
+        };
+        dma(0);
+        if (total > 1) dma(1);
+        if (total > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ws_barrier();                                             // P: raw(0) landed everywhere
+        split(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (total > 2) touch(2);
+        if (total > 3) touch(3);
+        for (int gs = 0; gs < total; ++gs) {
+            ws_barrier();                                         // B(gs)
+            if (gs + 2 < total) dma(gs + 2);                      // into the raw slot of raw(gs)
+            if (gs + 4 < total) touch(gs + 4);
+            if (gs + 1 < total) split(gs + 1);                    // raw(gs + 1) landed before B(gs)
+            // raw(gs + 2) landed; the newest touch may still fly
+            if (gs + 4 < total) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            if ((gs + 1) % nks == 0) ws_barrier();                // E of the compute waves' tile end
+        }
+        return;
+    }
+    // ------------------------------ compute ------------------------------
+    ws_barrier();                                                 // P
+    const int wm = wave & 1, wn = wave >> 1;
+    const int h1 = (tf1 + 1) >> 1, h2 = (tf2 + 1) >> 1;
+    const int o1 = 16 * h1 * wm, o2 = 16 * h2 * wn;
+    const int n1 = wm ? tf1 - h1 : h1, n2 = wn ? tf2 - h2 : h2;
+    for (int k = 0; k < nmine; ++k) {
+        const WsTile t = tile_at(k);
+        const int cw1 = W1 - (t.M0 + o1), cw2 = W2 - (t.N0 + o2);
+        const int v1 = cw1 <= 0 ? 0 : min(n1, (cw1 + 15) >> 4), v2 = cw2 <= 0 ? 0 : min(n2, (cw2 + 15) >> 4);
+        const int fa = v1 == 0 ? 0 : v2, fb = v1;
+        const int g0 = k * nks;
+        if (fa == 4) ws_tile_fb<4, MODE, NLM>(fb, a, smem, t, g0, nks, o1, o2, lane);
+        else if (fa == 3) ws_tile_fb<3, MODE, NLM>(fb, a, smem, t, g0, nks, o1, o2, lane);
+        else if (fa == 2) ws_tile_fb<2, MODE, NLM>(fb, a, smem, t, g0, nks, o1, o2, lane);
+        else if (fa == 1) ws_tile_fb<1, MODE, NLM>(fb, a, smem, t, g0, nks, o1, o2, lane);
+        else ws_tile<0, 1, MODE, NLM>(a, smem, t, g0, nks, o1, o2, lane);
+    }
+}
+#endif  // RAFTCORR_DEV
+
 }  // namespace rc
+
+#ifdef RAFTCORR_DEV
+static int device_cus_split() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+#endif
 
 // Split-bf16 build for fp32 fmaps and an fp32 pyramid.  Returns
 // hipErrorNotSupported (nothing launched) when the shape is outside what the
@@ -260,6 +525,27 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
     const long long nwg = (long long)a.B * a.H * tiles1 * tiles2;
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
+#ifdef RAFTCORR_DEV
+    // dev-only: RAFTCORR_SPLIT_KERNEL=3 runs the warp-specialised persistent
+    // kernel (measured and not kept) with the same
+    // RAFTCORR_SPLIT_MODE ablation flags
+    if (rc::dev_knob("RAFTCORR_SPLIT_KERNEL") == 3) {
+        const unsigned cus = (unsigned)device_cus_split();
+        const long long ntiles = nwg;
+        const unsigned nws = (unsigned)(ntiles < cus ? ntiles : cus);   // persistent: one workgroup per CU
+        switch (rc::dev_knob("RAFTCORR_SPLIT_MODE")) {
+            case 1: hipLaunchKernelGGL((rc::build_split_ws_kernel<1, 3>), dim3(nws), dim3(512), 0, s, a, (int)ntiles, tf1, tf2, tiles1, tiles2); break;
+            case 2: hipLaunchKernelGGL((rc::build_split_ws_kernel<2, 3>), dim3(nws), dim3(512), 0, s, a, (int)ntiles, tf1, tf2, tiles1, tiles2); break;
+            case 4: hipLaunchKernelGGL((rc::build_split_ws_kernel<4, 3>), dim3(nws), dim3(512), 0, s, a, (int)ntiles, tf1, tf2, tiles1, tiles2); break;
+            case 3: hipLaunchKernelGGL((rc::build_split_ws_kernel<3, 3>), dim3(nws), dim3(512), 0, s, a, (int)ntiles, tf1, tf2, tiles1, tiles2); break;
+            case 64: hipLaunchKernelGGL((rc::build_split_ws_kernel<64, 3>), dim3(nws), dim3(512), 0, s, a, (int)ntiles, tf1, tf2, tiles1, tiles2); break;
+            default:
+                if (a.nfused <= 3) hipLaunchKernelGGL((rc::build_split_ws_kernel<0, 3>), dim3(nws), dim3(512), 0, s, a, (int)ntiles, tf1, tf2, tiles1, tiles2);
+                else hipLaunchKernelGGL((rc::build_split_ws_kernel<0, rc::kSpMaxFused>), dim3(nws), dim3(512), 0, s, a, (int)ntiles, tf1, tf2, tiles1, tiles2);
+        }
+        return hipGetLastError();
+    }
+#endif
 #ifdef RAFTCORR_DEV
     // dev-only ablations (timing only): RAFTCORR_SPLIT_MODE = kMode* flags
     // (1 no operand loads, 2 no epilogue stores, 4 no MFMAs; sums combine)

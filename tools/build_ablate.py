@@ -47,15 +47,20 @@ def main():
     B, D, H, W1, W2, L, r, iters, _ = cfg
     dev = torch.device("cuda", 0)
     ll = a.config in bench.LOW_LATENCY_CONFIGS
-    variants = ["exact"] + [int(m) for m in a.modes.split(",") if m]
+    variants = ["exact", "ws"] + [int(m) for m in a.modes.split(",") if m]
     res = {str(v): [] for v in variants}
     with torch.no_grad():
         f1, f2, _ = bench.make_inputs(cfg, dev, seed=1)
 
         def run(v):
+            os.environ["RAFTCORR_SPLIT_KERNEL"] = "0"
             if v == "exact":
                 os.environ["RAFTCORR_SPLIT_MODE"] = "0"
                 return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll, exact_f32=True)
+            if v == "ws":           # the warp-specialised kernel (dev only, not kept)
+                os.environ["RAFTCORR_SPLIT_MODE"] = "0"
+                os.environ["RAFTCORR_SPLIT_KERNEL"] = "3"
+                return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
             os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
             return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
         for v in variants:
@@ -65,13 +70,15 @@ def main():
                 fn = run(v)
                 res[str(v)] += time_launches(fn, a.per)
         os.environ["RAFTCORR_SPLIT_MODE"] = "0"
+        os.environ["RAFTCORR_SPLIT_KERNEL"] = "0"
     out = {k: {"median_us": statistics.median(x), "min_us": min(x)} for k, x in res.items()}
     flops = bench.volume_flops(B, D, H, W1, W2)
     for k, v in out.items():
         v["fp32_equiv_tflops"] = flops / (v["median_us"] * 1e-6) / 1e12
     print(json.dumps({"config": a.config, "variants": out,
-                      "legend": "exact = fp32 MFMA ring; split modes: 0 product, 1 no loads, "
-                                "2 no stores, 4 no MFMA (sums combine)"}, indent=1))
+                      "legend": "exact = fp32 MFMA ring; ws = warp-specialised split kernel (not kept); split "
+                                "modes (build_split_kernel): 0 product, 1 no loads, 2 no stores, "
+                                "4 no MFMA (sums combine)"}, indent=1))
 
 
 if __name__ == "__main__":
