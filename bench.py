@@ -241,10 +241,15 @@ def e2e_pairs_per_s(cfg, device, steps, warmup, image_hw=(540, 960), mixed=False
 
 
 def backward_timing(cfg, f1, f2, coords, reps=3):
-    """Corr-path backward on the bench workload: per-kernel
-    event timing of rc_corr_lookup_backward (one per lookup call) and
-    rc_corr_build_backward, plus a whole autograd step (build + lookups +
-    backward through CorrBlock1D) with random output gradients."""
+    """Corr-path backward on the bench workload:
+    * the product lookup backward -- ONE rc_corr_lookup_backward_calls launch
+      summing all `iters` calls (what CorrBlock1D's autograd runs, DESIGN.md
+      §3.4c), event-timed;
+    * the per-call kernel (rc_corr_lookup_backward, one launch per call) and
+      its zeroed buffers, for comparison;
+    * rc_corr_build_backward;
+    * a whole autograd step (build + lookups + backward through CorrBlock1D)
+      with random output gradients."""
     from raft_stereo_amd import corr as rcorr
     B, D, H, W1, W2, L, r, iters, _ = cfg
     P = B * H * W1
@@ -252,67 +257,96 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
     widths = [W2 >> i for i in range(L)]
     g = torch.Generator().manual_seed(99)
     gouts = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(2)]
+    gl = [gouts[it % 2] for it in range(iters)]
     pair = rcorr._pair_grads_ok(L, r, W2)      # the layout CorrBlock1D's autograd uses
     grads = rcorr.grad_buffers(P, widths, dev, pair=pair)
+    cgrads = rcorr.grad_buffers(P, widths, dev, pair=pair, zero=False)
 
     def lbwd(c, go):
         rcorr.lookup_backward(grads, c, go, L, r)
 
+    def lcalls():
+        rcorr.lookup_backward_calls(cgrads, coords[:iters], gl, L, r, overwrite=True)
+
     for _ in range(2):   # warm-up
         lbwd(coords[0], gouts[0])
+        lcalls()
         rcorr.build_backward(f1, f2, grads)
-    lb, vb = [], []
+    lb, vb, lc = [], [], []
     for _ in range(reps):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 2)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 4)]
         ev[0].record()
         for it in range(iters):
             lbwd(coords[it], gouts[it % 2])
             ev[it + 1].record()
         rcorr.build_backward(f1, f2, grads)
         ev[iters + 1].record()
+        lcalls()
+        ev[iters + 2].record()
         torch.cuda.synchronize()
         lb += [ev[k].elapsed_time(ev[k + 1]) for k in range(iters)]
         vb.append(ev[iters].elapsed_time(ev[iters + 1]))
+        lc.append(ev[iters + 1].elapsed_time(ev[iters + 2]))
     lb_ms = sorted(lb)[len(lb) // 2]
     vb_ms = sorted(vb)[len(vb) // 2]
+    lc_ms = sorted(lc)[len(lc) // 2]
     # whole autograd step through the drop-in class
     a = f1.detach().clone().requires_grad_(True)
     b = f2.detach().clone().requires_grad_(True)
 
-    def train_step():
-        blk = CorrBlock1D(a, b, num_levels=L, radius=r)
+    def train_step(deferred=None):
+        blk = CorrBlock1D(a, b, num_levels=L, radius=r, grad_deferred=deferred)
         outs = [blk(coords[it]) for it in range(iters)]
-        torch.autograd.backward(outs, [gouts[it % 2] for it in range(iters)])
+        torch.autograd.backward(outs, gl)
 
-    train_step()
-    torch.cuda.synchronize()
-    steps = []
-    for _ in range(max(reps, 9)):     # median of synchronised single steps (host jitter)
-        t0 = time.perf_counter()
-        train_step()
+    def timed(fn):
+        fn()
         torch.cuda.synchronize()
-        steps.append((time.perf_counter() - t0) * 1e3)
-    step_ms = sorted(steps)[len(steps) // 2]
+        steps = []
+        for _ in range(max(reps, 9)):     # median of synchronised single steps (host jitter)
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            steps.append((time.perf_counter() - t0) * 1e3)
+        return sorted(steps)[len(steps) // 2]
+    step_ms = timed(train_step)
+    step_per_call_ms = timed(lambda: train_step(False))
     vflops = 2 * volume_flops(B, D, H, W1, W2)        # two GEMMs
-    # x, grad_out, per-level window RMW (the layout-independent definition of
-    # round 1; the pair layout's RMW touches 2 spans of 2(2r+4) elements instead)
+    # per-call kernel: x, grad_out, per-level window RMW (the layout-independent
+    # definition of round 1; the pair layout's RMW touches 2 spans of 2(2r+4))
     lbytes = P * (4 + L * (2 * r + 1) * 4 + 2 * L * (2 * r + 2) * 4)
-    return {"lookup_bwd_us": lb_ms * 1e3, "volume_bwd_us": vb_ms * 1e3,
-            "train_step_ms": step_ms, "train_pairs_per_s": B / (step_ms * 1e-3),
-            "roofline_volume_bwd": {"bound": "mfma", "achieved": vflops / (vb_ms * 1e-3) / 1e12,
-                                    "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                    "frac": vflops / (vb_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                                    "kernel": ("rc::volume_bwd_kernel<true,kPairFold>" if pair
-                                               else f"rc::volume_bwd_kernel<true,{L}>")},
-            "roofline_lookup_bwd": {"bound": "hbm", "achieved": lbytes / (lb_ms * 1e-3) / 1e9,
-                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                    "frac": lbytes / (lb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                    "algorithmic_bytes": lbytes,
-                                    "kernel": (f"rc::lookup_bwd_pair_kernel<{r},{L}>" if pair else
-                                               f"rc::lookup_bwd_pre_kernel<{r},{L}>" if r <= 4 and L <= 4
-                                               else f"rc::lookup_bwd_kernel<{r}>")},
-            "note": "step = CorrBlock1D build + lookups + autograd backward to both fmaps "
-                    "(random output gradients); kernel times are medians of event-timed launches"}
+    # all calls in one pass: every call's x and grad_out read once, the pair
+    # rows (16-B padded) written once
+    rows = sum(-(-(W2 >> l) // 4) * 4 for l in range(0, L, 2)) if pair else 0
+    cbytes = iters * P * (4 + L * (2 * r + 1) * 4) + P * rows * 4
+    out = {"lookup_bwd_calls_us": lc_ms * 1e3, "lookup_bwd_us": lb_ms * 1e3,
+           "volume_bwd_us": vb_ms * 1e3,
+           "train_step_ms": step_ms, "train_pairs_per_s": B / (step_ms * 1e-3),
+           "train_step_per_call_bwd_ms": step_per_call_ms,
+           "roofline_volume_bwd": {"bound": "mfma", "achieved": vflops / (vb_ms * 1e-3) / 1e12,
+                                   "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                   "frac": vflops / (vb_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                                   "kernel": ("rc::volume_bwd_kernel<true,kPairFold>" if pair
+                                              else f"rc::volume_bwd_kernel<true,{L}>")},
+           "roofline_lookup_bwd_per_call": {
+               "bound": "hbm", "achieved": lbytes / (lb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+               "unit": "GB/s", "frac": lbytes / (lb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+               "algorithmic_bytes": lbytes,
+               "kernel": (f"rc::lookup_bwd_pair_kernel<{r},{L}>" if pair else
+                          f"rc::lookup_bwd_pre_kernel<{r},{L}>" if r <= 4 and L <= 4
+                          else f"rc::lookup_bwd_kernel<{r}>")},
+           "note": "step = CorrBlock1D build + lookups + autograd backward to both fmaps "
+                   "(random output gradients; the lookup backward of all calls in one "
+                   "rc_corr_lookup_backward_calls pass, train_step_per_call_bwd_ms: one "
+                   "rc_corr_lookup_backward per call into zeroed buffers); kernel times are "
+                   "medians of event-timed launches"}
+    if pair:
+        out["roofline_lookup_bwd"] = {
+            "bound": "hbm", "achieved": cbytes / (lc_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": cbytes / (lc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "algorithmic_bytes": cbytes, "calls_per_launch": iters,
+            "kernel": f"rc::lookup_bwd_calls_kernel<{r},{L}>"}
+    return out
 
 
 def upsample_timing(cfg, device, reps=20):
@@ -638,14 +672,19 @@ def main():
     }
     if not args.no_backward and args.config == "sceneflow":
         result["backward"] = backward_timing(cfg, f1, f2, coords)
-        rl = result["backward"]["roofline_lookup_bwd"]
-        bname, bpmc = pmc_entry(pmc, rl["kernel"].split("<")[0])
-        if bpmc.get("hbm_bytes"):   # PMC bytes the lookup backward really moves, per launch
-            rl["kernel"] = bname
-            rl["traffic"] = bpmc["hbm_bytes"]
-            rl["traffic_gbs"] = rl["traffic"] / (result["backward"]["lookup_bwd_us"] * 1e-6) / 1e9
-            rl["traffic_frac"] = rl["traffic_gbs"] / HBM_PEAK_GBS
-            rl["traffic_over_algorithmic"] = rl["traffic"] / rl["algorithmic_bytes"]
+        bw = result["backward"]
+        for key, us in (("roofline_lookup_bwd", "lookup_bwd_calls_us"),
+                        ("roofline_lookup_bwd_per_call", "lookup_bwd_us")):
+            rl = bw.get(key)
+            if rl is None:
+                continue
+            bname, bpmc = pmc_entry(pmc, rl["kernel"].split("<")[0])
+            if bpmc.get("hbm_bytes"):   # PMC bytes the kernel really moves, per launch
+                rl["kernel"] = bname
+                rl["traffic"] = bpmc["hbm_bytes"]
+                rl["traffic_gbs"] = rl["traffic"] / (bw[us] * 1e-6) / 1e9
+                rl["traffic_frac"] = rl["traffic_gbs"] / HBM_PEAK_GBS
+                rl["traffic_over_algorithmic"] = rl["traffic"] / rl["algorithmic_bytes"]
         rv = result["backward"]["roofline_volume_bwd"]
         vbname, vbpmc = pmc_entry(pmc, "rc::volume_bwd_kernel")
         if "mfma_util" in vbpmc:    # the exact instance the backward ran (one per config)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 6
+#define RC_ABI_VERSION 7
 
 /* element types */
 #define RC_F32  0
@@ -210,6 +210,28 @@ int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long
                             int levels, int radius, const float *coords_x,
                             long coord_batch_stride, int B, int H, int W1,
                             const float *grad_out, void *stream);
+
+/* The gradients of n_calls lookups into the same gradient buffers, summed in
+ * one pass (ABI v7; model.py:376 runs the lookup `iters` times, and autograd
+ * adds every call's grid_sample input gradient, :275, into the levels):
+ * equal to n_calls rc_corr_lookup_backward calls up to the association of
+ * the fp32 sums.  coords_x[c], coord_batch_stride[c], grad_out[c]: call c's
+ * arguments as in rc_corr_lookup_backward (all calls share B, H, W1, levels,
+ * radius).  levels | RC_GRAD_OVERWRITE: the buffers receive the sum instead
+ * of having it added (they need not be zeroed first; row padding up to the
+ * next multiple of 4 columns is written as zeros).  With the pair layout and
+ * level-0 rows of at most ~1.5K floats at r = 4 the pixel's rows stay on chip
+ * while all calls accumulate, so each call's inputs are read once and each
+ * row written once; otherwise, and for the per-level
+ * layout, this is a loop over rc_corr_lookup_backward.  RC_SHADOW_LEVEL bits
+ * are RC_EUNSUPPORTED here.  RC_GRAD_OVERWRITE with n_calls == 0 is
+ * RC_EINVAL; n_calls == 0 otherwise does nothing. */
+#define RC_GRAD_OVERWRITE 0x40000
+int rc_corr_lookup_backward_calls(void *const *grad_pyr, const int *widths, const long *grad_ld,
+                                  int levels, int radius, int n_calls,
+                                  const float *const *coords_x, const long *coord_batch_stride,
+                                  int B, int H, int W1, const float *const *grad_out,
+                                  void *stream);
 
 /* Backward of rc_corr_build (model.py:284-295 pooling, :318-326 volume):
  *   Dl_{L-1} = grad_pyr[L-1], Dl_i[k] = grad_pyr[i][k] + Dl_{i+1}[k/2] / 2

@@ -17,10 +17,11 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 RC_F32, RC_BF16 = 0, 1
 RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
-ABI_VERSION = 6
+ABI_VERSION = 7
 RC_SHADOW = 0xFF00  # pyr_dtype flags: every stored level carries a line-phase shadow copy
 RC_OUT_CHANNELS_LAST = 0x10000   # pyr_dtype flag: NHWC lookup output (pair kernel)
 RC_BUILD_EXACT_F32 = 0x20000     # rc_corr_build flag: exact fp32 MFMA kernel instead of the split-bf16 one
+RC_GRAD_OVERWRITE = 0x40000      # rc_corr_lookup_backward_calls flag: write the sum, do not add
 
 
 def shadow_level(l):
@@ -50,6 +51,9 @@ SIGNATURES = {
                                  _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "rc_corr_lookup_backward": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l),
                                      _i, _i, _vp, _l, _i, _i, _i, _vp, _vp]),
+    "rc_corr_lookup_backward_calls": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_i), ctypes.POINTER(_l),
+                                           _i, _i, _i, ctypes.POINTER(_vp), ctypes.POINTER(_l), _i, _i,
+                                           _i, ctypes.POINTER(_vp), _vp]),
     "rc_convex_upsample": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rc_corr_build_backward": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_vp),
                                     ctypes.POINTER(_l), _i, _vp, _vp, _vp]),

@@ -348,9 +348,11 @@ class _GradLevels(list):
     shadow = frozenset()
 
 
-def grad_buffers(P, widths, device, pair=False, shadow=()):
+def grad_buffers(P, widths, device, pair=False, shadow=(), zero=True):
     """Zeroed fp32 level-gradient buffers (P, W_l) with rows padded to 16 bytes
     (the padding stays zero: rc_corr_lookup_backward never touches it).
+    ``zero=False``: uninitialised, for :func:`lookup_backward_calls` with
+    ``overwrite=True`` (which writes every row, padding included).
     ``pair``: the pair layout -- levels 1 and 3 are None, their gradients are
     folded into levels 0 and 2 by the pair backward kernel.  ``shadow``:
     levels (0 and/or 2 of the 4-level pair layout) whose allocation also holds
@@ -369,8 +371,10 @@ def grad_buffers(P, widths, device, pair=False, shadow=()):
         if l in shadow:
             total = _lib.shadow_offset(P, ld, 4) + P * ld * 4
             buf = torch.zeros(total // 4, dtype=torch.float32, device=device)[:P * ld].view(P, ld)
-        else:
+        elif zero:
             buf = torch.zeros((P, ld), dtype=torch.float32, device=device)
+        else:
+            buf = torch.empty((P, ld), dtype=torch.float32, device=device)
         bufs.append(buf[:, :W])
     bufs.shadow = shadow
     return bufs
@@ -405,6 +409,53 @@ def lookup_backward(grads, coords, grad_out, num_levels, radius):
             num_levels | _grad_shadow_flags(grads), radius, x.data_ptr(), cbs, B, H, W1, go.data_ptr(),
             _stream(coords.device))
     _lib.check(rc, "rc_corr_lookup_backward")
+
+
+def lookup_backward_calls(grads, coords_list, grad_out_list, num_levels, radius, overwrite=False):
+    """rc_corr_lookup_backward_calls: the gradients of several lookup calls
+    (``coords_list[c]``, ``grad_out_list[c]``) summed into ``grads`` in one
+    pass -- equal to calling :func:`lookup_backward` once per call up to the
+    association of the fp32 sums.  ``overwrite``: ``grads`` receive the sum
+    instead of having it added (RC_GRAD_OVERWRITE; they need not be zeroed,
+    see ``grad_buffers(zero=False)``).  With the pair layout the pixel's
+    gradient rows stay on chip across the calls."""
+    if len(coords_list) != len(grad_out_list):
+        raise ValueError("lookup_backward_calls: one grad_out per coords")
+    if getattr(grads, "shadow", ()):
+        raise ValueError("lookup_backward_calls: gradient shadow copies are not supported")
+    if not coords_list:
+        if overwrite:
+            for g in grads:
+                if g is not None:
+                    g.zero_()
+        return
+    xs, cbss, gos = [], [], []
+    for coords, grad_out in zip(coords_list, grad_out_list):
+        x, cbs = _check_coords(grads, coords)
+        B, _, H, W1 = coords.shape
+        go = grad_out.detach().float().contiguous()
+        if go.shape != (B, num_levels * (2 * radius + 1), H, W1):
+            raise RuntimeError(f"lookup_backward_calls: grad_out shape {tuple(go.shape)}")
+        xs.append(x)
+        cbss.append(cbs)
+        gos.append(go)
+    B, _, H, W1 = coords_list[0].shape
+    if any(tuple(c.shape) != tuple(coords_list[0].shape) for c in coords_list):
+        raise RuntimeError("lookup_backward_calls: every call needs the same coords shape")
+    if B * H * W1 == 0:
+        return
+    W0 = grads[0].shape[-1]
+    g = [grads[i] for i in range(num_levels)]
+    flags = num_levels | (_lib.RC_GRAD_OVERWRITE if overwrite else 0)
+    with torch.cuda.device(coords_list[0].device):
+        rc = _lib.lib().rc_corr_lookup_backward_calls(
+            _lib.ptr_array([None if t is None else t.data_ptr() for t in g]),
+            _lib.int_array([W0 >> i for i in range(num_levels)]),
+            _lib.long_array([W0 >> i if t is None else t.stride(0) for i, t in enumerate(g)]),
+            flags, radius, len(xs), _lib.ptr_array([x.data_ptr() for x in xs]),
+            _lib.long_array(cbss), B, H, W1, _lib.ptr_array([go.data_ptr() for go in gos]),
+            _stream(coords_list[0].device))
+    _lib.check(rc, "rc_corr_lookup_backward_calls")
 
 
 def build_backward(fmap1, fmap2, grads):
@@ -471,24 +522,43 @@ def _check_grad_shadow(grad_shadow, num_levels, radius, W0):
 class _GradState:
     """Level gradients shared by one CorrBlock1D's lookup nodes and its build
     node.  Holds no pyramid and no graph node, so no reference cycle keeps the
-    pyramid alive."""
+    pyramid alive.
 
-    def __init__(self, P, widths, device, num_levels, radius, grad_shadow=None):
+    With the pair layout and no gradient shadow copies, the lookup nodes only
+    record their (coords, grad_out); the build node sums all of them in one
+    rc_corr_lookup_backward_calls pass (``deferred``) into
+    buffers it never zeroes.  Otherwise each lookup node adds its call into
+    zeroed buffers right away (rc_corr_lookup_backward)."""
+
+    def __init__(self, P, widths, device, num_levels, radius, grad_shadow=None, deferred=None):
         self.P, self.widths, self.device = P, widths, device
         self.num_levels, self.radius = num_levels, radius
         self.pair = _pair_grads_ok(num_levels, radius, widths[0])
         if grad_shadow is None:
             grad_shadow = default_grad_shadow_levels(P, widths, num_levels, self.pair)
         self.grad_shadow = frozenset(grad_shadow) if self.pair and num_levels == 4 else frozenset()
+        if deferred is None:
+            deferred = self.pair and not self.grad_shadow
+        self.deferred = bool(deferred) and self.pair and not self.grad_shadow
         self.grads = None
+        self.pending = []
 
     def accumulate(self, coords, grad_out):
+        if self.deferred:
+            self.pending.append((coords, grad_out))
+            return
         if self.grads is None:
             self.grads = grad_buffers(self.P, self.widths, self.device, pair=self.pair,
                                       shadow=self.grad_shadow)
         lookup_backward(self.grads, coords, grad_out, self.num_levels, self.radius)
 
     def take(self):
+        if self.pending:
+            calls, self.pending = self.pending, []
+            grads = grad_buffers(self.P, self.widths, self.device, pair=True, zero=False)
+            lookup_backward_calls(grads, [c for c, _ in calls], [g for _, g in calls],
+                                  self.num_levels, self.radius, overwrite=True)
+            return grads
         g, self.grads = self.grads, None
         return g
 
@@ -533,7 +603,7 @@ class CorrBlock1D:
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
                  lazy_levels=None, shadow=None, channels_last=False, low_latency=False,
-                 grad_shadow=None, exact_f32=False):
+                 grad_shadow=None, exact_f32=False, grad_deferred=None):
         self.num_levels = num_levels
         self.radius = radius
         # lookup outputs in NHWC memory order (torch.channels_last): same
@@ -569,6 +639,9 @@ class CorrBlock1D:
         # §3.2g): a shorter dependent chain per launch, bit-identical values
         # grad_shadow: levels (0, 2 of the 4-level pair layout) whose gradient
         # buffers get an RC_SHADOW copy; None = the default
+        # grad_deferred: the lookup nodes record their inputs and the build
+        # node sums every call in one pass; None = on
+        # wherever the pair gradient layout applies (no gradient shadow copies)
         if low_latency:
             self._chain = False
         lazy = self._chain if lazy_levels is None else (bool(lazy_levels) and self._chain)
@@ -605,7 +678,8 @@ class CorrBlock1D:
         self._state = self._token = None
         if grad:
             self._state = _GradState(B * H * W1, [W2 >> i for i in range(num_levels)],
-                                     fmap1.device, num_levels, radius, grad_shadow)
+                                     fmap1.device, num_levels, radius, grad_shadow,
+                                     deferred=grad_deferred)
             self._token = _BuildFn.apply(fmap1, fmap2, self._state)
 
     @property

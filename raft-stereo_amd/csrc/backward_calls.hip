@@ -1,0 +1,257 @@
+// Deferred lookup backward (gfx950): the level gradients of ALL lookup calls
+// of one CorrBlock1D summed in one pass, SURVEY.md §8f rank 2.
+//
+// The reference runs grid_sample's input gradient (model.py:275) once per
+// lookup call (:376, `iters` calls) and autograd adds the results into the
+// pyramid levels' gradients, then through avg_pool2d's backward (:294).
+// lookup_bwd_pair_kernel (backward.hip) does that per call: each call
+// read-modify-writes two spans of every pixel's gradient rows in HBM (~724 B
+// of traffic per pixel and call at config 2, 1.55x its algorithmic bytes,
+// because 16-B chunks of per-pixel rows cost whole lines).
+//
+// This kernel keeps the pixel's whole pair-layout gradient rows -- level 0
+// (with level 1 folded in, c/2 to both children) and level 2 (with level 3)
+// -- in LDS while it walks the calls, so HBM sees each call's coordinates and
+// output gradients once (coalesced, 4 + L(2r+1)*4 B per pixel) and each row
+// written once at the end (no zeroing pass, no read-modify-write):
+//
+//   workgroup = `pix` consecutive pixels x NL/2 level pairs, one lane per
+//   (pixel, pair); lane (k, i) owns LDS row i of pair k.  Per call the lane
+//   sums its 2(2r+1) taps into two register strips -- s0 over level-2k
+//   elements n-r..n+r+1 (n = floor(x/2^2k)), s1 over level-(2k+1) elements
+//   m-r..m+r+1 (m = floor(x/2^(2k+1))) -- with static indices, then adds s1
+//   to LDS elements 2(m-r)+2j, +1 (8-B aligned ds ops) and s0 to n-r+j.
+//   Elements outside [0, W) get exactly +0.0 (masked), so the strips need no
+//   per-element guard: rows are separated by margins of 4r+4 floats that
+//   receive only +0.0 from the lanes on either side (racing writes of equal
+//   values) and that the write-back never copies.
+//
+// A lane takes that strip path when every tap sits where the exact
+// arithmetic puts it (floor of the unnormalised tap = n-r+t at level 2k,
+// m-r+t at level 2k+1) and n - 2m is 0 or 1; otherwise (rounding at integer
+// x, subnormal x) it adds tap by tap to in-range elements, the per-call
+// kernel's order.  Sums differ from the per-call kernel only in association
+// (tolerance-level parity, tests/test_backward_calls_gpu.py).
+//
+// Loads: four calls in flight per lane (19 dwords each) while the current
+// one is summed; calls past the last reload the last one (no branch around
+// a load, so the wait counts stay static).
+#include "common.h"
+
+namespace rc {
+
+extern __shared__ float bwd_calls_lds[];
+
+template <int R>
+struct BwdCall {
+    float x;
+    float gv[2][2 * R + 1];   // output gradients of levels 2k and 2k+1
+};
+
+template <int R>
+__device__ __forceinline__ void bwd_call_load(BwdCall<R> &c, const LookupBwdCallsArgs &a, int call,
+                                              long long bimg, long long rem, long long go_off) {
+    constexpr int T = 2 * R + 1;
+    c.x = a.coords[call][bimg * a.cbs[call] + rem];
+    const float *go = a.grad_out[call] + go_off;
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int t = 0; t < T; ++t) c.gv[e][t] = go[(long long)(e * T + t) * a.HW];
+}
+
+struct PairGeom {
+    int Wlo, Whi;
+    float slo, shi;       // 2^-2k, 2^-(2k+1)
+    float halflo, halfhi; // (W-1)/2
+    DivRN dvlo, dvhi;     // division by W-1
+};
+
+// grid_sample's unnormalised tap position (model.py:271-275 with
+// align_corners=True), the forward's exact arithmetic.
+__device__ __forceinline__ float tap_pos(float xl, int t_minus_r, const DivRN &dv, float half) {
+    return ((div_rn(2.0f * ((float)t_minus_r + xl), dv) - 1.0f) + 1.0f) * half;
+}
+
+template <int R>
+__device__ __forceinline__ void bwd_call_add(const BwdCall<R> &c, float *row, const PairGeom &g) {
+    constexpr int T = 2 * R + 1, NJ = 2 * R + 2;
+    const float xlo = c.x * g.slo, xhi = c.x * g.shi;
+    if (!(xhi > -(float)(R + 4) && xhi < (float)(g.Whi + R + 4))) return;   // also NaN
+    const float mf = floorf(xhi), nf = floorf(xlo);
+    const int m = (int)mf, n = (int)nf;
+    if (m < -R - 2 || m > g.Whi + R) return;   // every tap of both levels outside the row
+    const int dd = n - 2 * m;
+    bool fast = dd == 0 || dd == 1;
+    float s0[NJ], s1[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s0[j] = s1[j] = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xp = e ? tap_pos(xhi, t - R, g.dvhi, g.halfhi) : tap_pos(xlo, t - R, g.dvlo, g.halflo);
+            const float x0 = floorf(xp);
+            const float gv = c.gv[e][t];
+            const float c1 = (xp - x0) * gv, c0 = ((x0 + 1.0f) - xp) * gv;   // ne / nw corners
+            fast = fast && (x0 == (e ? mf : nf) + (float)(t - R));
+            if (e == 0) {
+                s0[t] += c0;
+                s0[t + 1] += c1;
+            } else {                       // avg_pool2d's backward: c/2 to both children
+                s1[t] += c0 * 0.5f;
+                s1[t + 1] += c1 * 0.5f;
+            }
+        }
+    }
+    if (fast) {
+        const int jb = m - R, ib = n - R;
+        f32x2 *q = reinterpret_cast<f32x2 *>(row + 2 * jb);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int jj = jb + j;
+            const float v = (jj >= 0 && jj < g.Whi) ? s1[j] : 0.0f;
+            f32x2 w = q[j];
+            w[0] += v;
+            w[1] += v;
+            q[j] = w;
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int ii = ib + j;
+            row[ib + j] += (ii >= 0 && ii < g.Wlo) ? s0[j] : 0.0f;
+        }
+        return;
+    }
+    // tap by tap, in-range elements only
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int W = e ? g.Whi : g.Wlo;
+        const float Wm1 = (float)(W - 1);
+        for (int t = 0; t < T; ++t) {
+            const float xp = e ? tap_pos(xhi, t - R, g.dvhi, g.halfhi) : tap_pos(xlo, t - R, g.dvlo, g.halflo);
+            const float x0 = floorf(xp);
+            const float gv = c.gv[e][t];
+            const float c1 = (xp - x0) * gv, c0 = ((x0 + 1.0f) - xp) * gv;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const float xe = x0 + (float)s;
+                if (!(xe >= 0.0f && xe <= Wm1)) continue;
+                const float cc = s ? c1 : c0;
+                const int k = (int)xe;
+                if (e == 0) {
+                    row[k] += cc;
+                } else {
+                    row[2 * k] += cc * 0.5f;
+                    row[2 * k + 1] += cc * 0.5f;
+                }
+            }
+        }
+    }
+}
+
+// NL = 2 (one level pair) or 4 (two); blockDim = pix * NL / 2.
+template <int R, int NL>
+__global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArgs a) {
+    constexpr int NP = NL / 2, T = 2 * R + 1;
+    float *lds = bwd_calls_lds;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const long long pblk = (long long)blockIdx.x * a.pix;
+    const int npix = (int)min((long long)a.pix, a.P - pblk);
+    for (int f = 4 * tid; f < a.lds_floats; f += 4 * nthr)
+        *reinterpret_cast<f32x4 *>(lds + f) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    __syncthreads();
+
+    const int k = tid / a.pix, i = tid - k * a.pix;
+    if (k < NP && i < npix) {
+        const int lo = 2 * k;
+        PairGeom g;
+        g.Wlo = a.W[lo];
+        g.Whi = a.W[lo + 1];
+        g.slo = 1.0f / (float)(1 << lo);
+        g.shi = 0.5f * g.slo;
+        g.halflo = (float)(g.Wlo - 1) / 2.0f;
+        g.halfhi = (float)(g.Whi - 1) / 2.0f;
+        g.dvlo = div_prep((float)(g.Wlo - 1));
+        g.dvhi = div_prep((float)(g.Whi - 1));
+        float *row = lds + a.rowbase[k] + i * a.S[k];
+        const long long p = pblk + i, bimg = p / a.HW, rem = p - bimg * a.HW;
+        const long long go_off = (bimg * (NL * T) + lo * T) * (long long)a.HW + rem;
+        const int last = a.ncalls - 1;
+        BwdCall<R> b0, b1, b2, b3;
+        bwd_call_load<R>(b0, a, 0, bimg, rem, go_off);
+        bwd_call_load<R>(b1, a, min(1, last), bimg, rem, go_off);
+        bwd_call_load<R>(b2, a, min(2, last), bimg, rem, go_off);
+        bwd_call_load<R>(b3, a, min(3, last), bimg, rem, go_off);
+        for (int c = 0; c < a.ncalls; c += 4) {
+            bwd_call_add<R>(b0, row, g);
+            bwd_call_load<R>(b0, a, min(c + 4, last), bimg, rem, go_off);
+            if (c + 1 < a.ncalls) bwd_call_add<R>(b1, row, g);
+            bwd_call_load<R>(b1, a, min(c + 5, last), bimg, rem, go_off);
+            if (c + 2 < a.ncalls) bwd_call_add<R>(b2, row, g);
+            bwd_call_load<R>(b2, a, min(c + 6, last), bimg, rem, go_off);
+            if (c + 3 < a.ncalls) bwd_call_add<R>(b3, row, g);
+            bwd_call_load<R>(b3, a, min(c + 7, last), bimg, rem, go_off);
+        }
+    }
+    __syncthreads();
+
+    // write back: one wave per row, 16-B chunks along the row (coalesced)
+    const int lane = tid & 63, wave = tid >> 6, nwave = (nthr + 63) >> 6;
+#pragma unroll
+    for (int kk = 0; kk < NP; ++kk) {
+        const int n4 = a.wout[kk] >> 2;
+        for (int r = wave; r < npix; r += nwave) {
+            const f32x4 *src = reinterpret_cast<const f32x4 *>(lds + a.rowbase[kk] + r * a.S[kk]);
+            f32x4 *dst = reinterpret_cast<f32x4 *>(a.g[kk] + (pblk + r) * a.ld[kk]);
+            for (int c4 = lane; c4 < n4; c4 += 64) {
+                f32x4 v = src[c4];
+                if (a.accumulate) v += dst[c4];
+                dst[c4] = v;
+            }
+        }
+    }
+}
+
+}  // namespace rc
+
+// LDS per workgroup: pair k holds pix rows of S_k = round4(W_2k) + M floats
+// after a leading margin M = 4r+4 (the strips' reach past either end of a
+// row); pix is the largest of 64/(NL/2), ..., 8 pixels whose rows fit 64 KB.
+hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int levels, hipStream_t s) {
+    if (a.P <= 0 || a.ncalls <= 0) return hipSuccess;
+    if (a.ncalls > rc::kMaxBwdCalls || (levels != 2 && levels != 4) || radius < 1 || radius > 4)
+        return hipErrorInvalidValue;
+    const int np = levels / 2, M = 4 * radius + 4;
+    int per_pix = 0;
+    for (int k = 0; k < np; ++k) {
+        const int w4 = (a.W[2 * k] + 3) & ~3;
+        a.S[k] = w4 + M;
+        a.wout[k] = w4;
+        per_pix += a.S[k];
+    }
+    int pix = 64 / np;
+    while (pix > 8 && (long long)(per_pix * pix + np * M) * 4 > 65536) pix >>= 1;
+    if ((long long)(per_pix * pix + np * M) * 4 > 65536) return hipErrorNotSupported;
+    a.pix = pix;
+    int off = 0;
+    for (int k = 0; k < np; ++k) {
+        a.rowbase[k] = off + M;
+        off += M + pix * a.S[k];
+    }
+    a.lds_floats = (off + 3) & ~3;
+    const unsigned nblk = (unsigned)((a.P + pix - 1) / pix);
+    const size_t lds = (size_t)a.lds_floats * 4;
+    const dim3 blk(pix * np);
+#define RC_LBWDC(RR)                                                                                      \
+    if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<RR, 4>), dim3(nblk), blk, lds, s, a); \
+    else hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<RR, 2>), dim3(nblk), blk, lds, s, a);
+    switch (radius) {
+        case 1: RC_LBWDC(1) break;
+        case 2: RC_LBWDC(2) break;
+        case 3: RC_LBWDC(3) break;
+        case 4: RC_LBWDC(4) break;
+    }
+#undef RC_LBWDC
+    return hipGetLastError();
+}

@@ -4,6 +4,7 @@
 // (e.g. W2 < 2^num_levels makes avg_pool2d raise at model.py:294), then
 // launches on the caller's stream.  Nothing here allocates or synchronises, so
 // every entry point is safe inside hipStreamBeginCapture.
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -361,58 +362,55 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
                   "rc_corr_lookup_step: launch");
 }
 
-extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
-                                       const long *grad_ld, int levels, int radius,
-                                       const float *coords_x, long coord_batch_stride, int B,
-                                       int H, int W1, const float *grad_out, void *stream) {
-    g_err[0] = 0;
+namespace {
+// Validation shared by rc_corr_lookup_backward and rc_corr_lookup_backward_calls.
+int prep_lookup_bwd(const char *who, void *const *grad_pyr, const int *widths, const long *grad_ld,
+                    int levels, int radius, const float *coords_x, long coord_batch_stride, int B,
+                    int H, int W1, const float *grad_out, rc::LookupBwdArgs &a, bool *empty,
+                    bool *pair_out) {
     // RC_SHADOW_LEVEL(l) bits above the level count: gradient copies (pair layout)
     const unsigned shmask = ((unsigned)levels >> 8) & 0xFFu;
     levels &= 0xFF;
     rc::LookupArgs la;
-    bool empty;
-    int rc = prep_lookup("rc_corr_lookup_backward", grad_pyr, widths, grad_ld, RC_F32, levels,
-                         radius, coords_x, coord_batch_stride, B, H, W1, grad_out, la, &empty, true);
-    if (rc || empty) return rc;
+    int rc = prep_lookup(who, grad_pyr, widths, grad_ld, RC_F32, levels, radius, coords_x,
+                         coord_batch_stride, B, H, W1, grad_out, la, empty, true);
+    if (rc || *empty) return rc;
     // pair-folded buffers: levels 1 and 3 NULL, their gradients folded into
     // levels 0 and 2 (2 or 4 levels, radius 1..4, widths halving, W <= 2^16)
     const bool pair = levels >= 2 && !grad_pyr[1];
+    *pair_out = pair;
     if (pair) {
         bool ok = (levels == 2 || (levels == 4 && grad_pyr[2] && !grad_pyr[3])) && radius <= 4 &&
                   widths[0] <= 65536;
         for (int i = 1; i < levels; ++i) ok = ok && widths[i] == widths[i - 1] / 2;
         if (!ok)
-            return fail(RC_EINVAL, "rc_corr_lookup_backward: NULL gradient levels need the pair "
-                        "layout (levels 2 or 4, level 1 [and 3] NULL, radius <= 4, halving widths)");
+            return fail(RC_EINVAL, "%s: NULL gradient levels need the pair layout (levels 2 or 4, "
+                        "level 1 [and 3] NULL, radius <= 4, halving widths)", who);
         if (shmask && (levels != 4 || (shmask & ~0x5u)))
-            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_backward: RC_SHADOW gradient copies are "
-                        "levels 0 and 2 of the 4-level pair layout");
+            return fail(RC_EUNSUPPORTED, "%s: RC_SHADOW gradient copies are levels 0 and 2 of the "
+                        "4-level pair layout", who);
     } else if (shmask) {
-        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_backward: RC_SHADOW needs the pair layout");
+        return fail(RC_EUNSUPPORTED, "%s: RC_SHADOW needs the pair layout", who);
     } else {
         for (int i = 1; i < levels; ++i)
-            if (!grad_pyr[i])
-                return fail(RC_EINVAL, "rc_corr_lookup_backward: level %d null", i);
+            if (!grad_pyr[i]) return fail(RC_EINVAL, "%s: level %d null", who, i);
     }
-    rc::LookupBwdArgs a{};
+    a = rc::LookupBwdArgs{};
     for (int i = 0; i < levels; ++i) {
+        a.W[i] = la.W[i];
+        a.ld[i] = la.ld[i];
         if (!grad_pyr[i]) {
             a.g[i] = nullptr;
-            a.W[i] = la.W[i];
-            a.ld[i] = la.ld[i];
             continue;
         }
         if (la.ld[i] % 4 != 0)
-            return fail(RC_EINVAL, "rc_corr_lookup_backward: row stride %lld of level %d is not a "
-                        "multiple of 4", la.ld[i], i);
+            return fail(RC_EINVAL, "%s: row stride %lld of level %d is not a multiple of 4", who,
+                        la.ld[i], i);
         a.g[i] = static_cast<float *>(const_cast<void *>(la.lvl[i]));
-        a.W[i] = la.W[i];
-        a.ld[i] = la.ld[i];
         if (shmask >> i & 1u) {
             a.shadow[i] = shadow_offset(la.P, la.ld[i], 4);
             if (a.shadow[i] + la.P * la.ld[i] * 4 > 0xFFFFFF00LL)
-                return fail(RC_EUNSUPPORTED, "rc_corr_lookup_backward: level %d with its shadow copy "
-                            "exceeds 4 GiB", i);
+                return fail(RC_EUNSUPPORTED, "%s: level %d with its shadow copy exceeds 4 GiB", who, i);
         }
     }
     a.coords = coords_x;
@@ -421,8 +419,91 @@ extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
     a.P = la.P;
     a.HW = la.HW;
     a.levels = levels;
+    return RC_OK;
+}
+}  // namespace
+
+extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
+                                       const long *grad_ld, int levels, int radius,
+                                       const float *coords_x, long coord_batch_stride, int B,
+                                       int H, int W1, const float *grad_out, void *stream) {
+    g_err[0] = 0;
+    rc::LookupBwdArgs a;
+    bool empty = false, pair = false;
+    int rc = prep_lookup_bwd("rc_corr_lookup_backward", grad_pyr, widths, grad_ld, levels, radius,
+                             coords_x, coord_batch_stride, B, H, W1, grad_out, a, &empty, &pair);
+    if (rc || empty) return rc;
     return hip_rc(rc_launch_lookup_bwd(a, radius, reinterpret_cast<hipStream_t>(stream)),
                   "rc_corr_lookup_backward: launch");
+}
+
+extern "C" int rc_corr_lookup_backward_calls(void *const *grad_pyr, const int *widths,
+                                             const long *grad_ld, int levels, int radius,
+                                             int n_calls, const float *const *coords_x,
+                                             const long *coord_batch_stride, int B, int H, int W1,
+                                             const float *const *grad_out, void *stream) {
+    g_err[0] = 0;
+    const char *who = "rc_corr_lookup_backward_calls";
+    const bool overwrite = (levels & RC_GRAD_OVERWRITE) != 0;
+    levels &= ~RC_GRAD_OVERWRITE;
+    if (n_calls < 0) return fail(RC_EINVAL, "%s: n_calls=%d", who, n_calls);
+    if (n_calls > 0 && (!coords_x || !coord_batch_stride || !grad_out))
+        return fail(RC_EINVAL, "%s: null coords / stride / grad_out array", who);
+    if (levels & 0xFF00) return fail(RC_EUNSUPPORTED, "%s: RC_SHADOW gradient copies", who);
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    rc::LookupBwdArgs a;
+    bool empty = false, pair = false;
+    for (int c = 0; c < n_calls; ++c) {       // every call validated before any launch
+        int rc = prep_lookup_bwd(who, grad_pyr, widths, grad_ld, levels, radius, coords_x[c],
+                                 coord_batch_stride[c], B, H, W1, grad_out[c], a, &empty, &pair);
+        if (rc || empty) return rc;
+    }
+    if (n_calls == 0) {
+        if (overwrite) return fail(RC_EINVAL, "%s: RC_GRAD_OVERWRITE with no calls", who);
+        return RC_OK;
+    }
+    auto per_call = [&]() -> int {
+        // per-level layout, or rows too wide for LDS: zero if asked, then one
+        // rc_corr_lookup_backward launch per call
+        if (overwrite)
+            for (int i = 0; i < a.levels; ++i)
+                if (a.g[i]) {
+                    hipError_t e = hipMemsetAsync(a.g[i], 0, (size_t)(a.P * a.ld[i]) * 4, s);
+                    if (e != hipSuccess) return hip_rc(e, "rc_corr_lookup_backward_calls: memset");
+                }
+        for (int c = 0; c < n_calls; ++c) {
+            a.coords = coords_x[c];
+            a.cbs = coord_batch_stride[c];
+            a.grad_out = grad_out[c];
+            hipError_t e = rc_launch_lookup_bwd(a, radius, s);
+            if (e != hipSuccess) return hip_rc(e, "rc_corr_lookup_backward_calls: launch");
+        }
+        return RC_OK;
+    };
+    if (!pair) return per_call();
+    rc::LookupBwdCallsArgs ca{};
+    ca.g[0] = a.g[0];
+    ca.ld[0] = a.ld[0];
+    if (a.levels == 4) {
+        ca.g[1] = a.g[2];
+        ca.ld[1] = a.ld[2];
+    }
+    for (int i = 0; i < a.levels; ++i) ca.W[i] = a.W[i];
+    ca.P = a.P;
+    ca.HW = a.HW;
+    for (int c0 = 0; c0 < n_calls; c0 += rc::kMaxBwdCalls) {
+        ca.ncalls = std::min(rc::kMaxBwdCalls, n_calls - c0);
+        ca.accumulate = (c0 > 0 || !overwrite) ? 1 : 0;
+        for (int c = 0; c < ca.ncalls; ++c) {
+            ca.coords[c] = coords_x[c0 + c];
+            ca.cbs[c] = coord_batch_stride[c0 + c];
+            ca.grad_out[c] = grad_out[c0 + c];
+        }
+        hipError_t e = rc_launch_lookup_bwd_calls(ca, radius, a.levels, s);
+        if (e == hipErrorNotSupported && c0 == 0) return per_call();   // nothing launched yet
+        if (e != hipSuccess) return hip_rc(e, "rc_corr_lookup_backward_calls: launch");
+    }
+    return RC_OK;
 }
 
 extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int fmap_dtype, int B,

@@ -144,6 +144,27 @@ struct LookupBwdArgs {
     long long shadow[kMaxLevels];   // bytes from g[l] to its RC_SHADOW copy (pair layout), 0 = none
 };
 
+// Deferred lookup backward (backward_calls.hip): the gradients of up to
+// kMaxBwdCalls lookup calls summed into pair-layout buffers in one pass.
+constexpr int kMaxBwdCalls = 32;
+struct LookupBwdCallsArgs {
+    float *g[2];              // level 0 and level 2 gradient rows (pair layout)
+    long long ld[2];          // their row strides (floats, % 4 == 0)
+    int W[4];                 // level widths W0 >> l
+    int wout[2];              // columns written back per row (round4(W), <= ld)
+    int rowbase[2];           // LDS float offset of row 0, element 0, of pair k
+    int S[2];                 // LDS row stride (floats) of pair k
+    int lds_floats;           // LDS floats zeroed per workgroup (% 4 == 0)
+    int pix;                  // pixels per workgroup
+    int ncalls;               // 1..kMaxBwdCalls
+    int accumulate;           // 0: overwrite the rows; 1: add to them
+    long long P;
+    int HW;
+    const float *coords[kMaxBwdCalls];
+    long long cbs[kMaxBwdCalls];
+    const float *grad_out[kMaxBwdCalls];   // [B][levels*(2r+1)][H][W1]
+};
+
 // Backward of the build: level gradients -> feature-map gradients (fp32).
 struct BuildBwdArgs {
     const float *f1, *f2;     // [B][D][H][W1], [B][D][H][W2]
@@ -173,6 +194,8 @@ hipError_t rc_launch_lookup_conv(const rc::LookupArgs &a, int radius, int pyr_bf
 hipError_t rc_launch_lookup_chain(const rc::LookupArgs &a, int radius, hipStream_t s);
 hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s);
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
+// fills a.pix / rowbase / S / lds_floats from W, radius, levels
+hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int levels, hipStream_t s);
 hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s);
 hipError_t rc_launch_convex_upsample(const float *flow, const float *mask, int N, int C, int H,
                                      int W, int factor, float *out, hipStream_t s);

@@ -90,4 +90,22 @@ if has pmcv; then
         --output-format csv -d "$OUT/pmc_v2" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
     python tools/pmc_raw.py "$OUT/pmc_v1" > "$OUT/pmc_v.txt" 2>&1; python tools/pmc_raw.py "$OUT/pmc_v2" >> "$OUT/pmc_v.txt" 2>&1; cat "$OUT/pmc_v.txt"
 fi
+if has calib; then   # FETCH_SIZE / WRITE_SIZE per byte for scattered 64-256 B rows
+    step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o f \
+        -- python3 tools/pmc_calib_random.py
+    step calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib_write" -o w \
+        -- python3 tools/pmc_calib_random.py
+    python tools/pmc_calib_report.py "$OUT/calib_fetch" "$OUT/calib_write" > "$OUT/calib.txt" 2>&1; cat "$OUT/calib.txt"
+fi
+if has pmcjson; then   # profiles/pmc.json: three counter passes of bench.py itself per config
+    for C in ${PMC_CONFIGS:-sceneflow kitti middlebury realtime}; do
+        BA="--config $C --pmc-calibrate --steps 2 --warmup 1 --no-cpu-baseline --e2e-steps 0"
+        step pmcj_${C}_f 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcj_${C}_f" -o f -- python3 bench.py $BA
+        step pmcj_${C}_w 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcj_${C}_w" -o w -- python3 bench.py $BA
+        step pmcj_${C}_s 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES \
+            --output-format csv -d "$OUT/pmcj_${C}_s" -o s -- python3 bench.py $BA
+        python tools/pmc_collect.py $C "$OUT/pmcj_${C}_f" "$OUT/pmcj_${C}_w" "$OUT/pmcj_${C}_s" \
+            --out "$OUT/pmc.json" --tag "$TAG" > "$OUT/pmcj_${C}.txt" 2>&1; cat "$OUT/pmcj_${C}.txt"
+    done
+fi
 exit 0
