@@ -300,14 +300,20 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
         torch.autograd.backward(outs, gl)
 
     def timed(fn):
+        # median over synchronised single steps of the GPU time between two
+        # events around the step (host-side jitter of one step, e.g. an
+        # allocator call, stays out of the median)
         fn()
         torch.cuda.synchronize()
         steps = []
-        for _ in range(max(reps, 9)):     # median of synchronised single steps (host jitter)
-            t0 = time.perf_counter()
-            fn()
+        for _ in range(max(reps, 9)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
-            steps.append((time.perf_counter() - t0) * 1e3)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            steps.append(e0.elapsed_time(e1))
         return sorted(steps)[len(steps) // 2]
     step_ms = timed(train_step)
     step_per_call_ms = timed(lambda: train_step(False))

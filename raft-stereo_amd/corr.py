@@ -542,6 +542,13 @@ class _GradState:
         self.deferred = bool(deferred) and self.pair and not self.grad_shadow
         self.grads = None
         self.pending = []
+        self.token_sent = False
+
+    def token_grad(self, device):
+        if self.token_sent:
+            return None
+        self.token_sent = True
+        return torch.zeros((), dtype=torch.float32, device=device)
 
     def accumulate(self, coords, grad_out):
         if self.deferred:
@@ -577,6 +584,7 @@ class _BuildFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _token_grad):
         f1, f2 = ctx.saved_tensors
+        ctx.state.token_sent = False          # a later backward through a new graph
         grads = ctx.state.take()
         if grads is None:          # no lookup output reached the loss
             return None, None, None
@@ -595,7 +603,10 @@ class _LookupFn(torch.autograd.Function):
     def backward(ctx, grad_out):
         (coords,) = ctx.saved_tensors
         ctx.state.accumulate(coords, grad_out)
-        return torch.zeros((), dtype=torch.float32, device=coords.device), None, None, None
+        # the build node only needs SOME defined gradient on its token: the
+        # first lookup node to run hands over one zero, the others None (no
+        # fill and no add kernel per call)
+        return ctx.state.token_grad(coords.device), None, None, None
 
 
 class CorrBlock1D:

@@ -36,6 +36,10 @@
 // Loads: four calls in flight per lane (19 dwords each) while the current
 // one is summed; calls past the last reload the last one (no branch around
 // a load, so the wait counts stay static).
+//
+// Measured and not kept: the row updates as LDS-side adds (ds_add_f32, no
+// read on the lane's chain; same order): 2499 vs 669 us per 32-call launch
+// at config 2 (r03m).
 #include "common.h"
 
 namespace rc {
@@ -197,14 +201,16 @@ __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArg
     __syncthreads();
 
     // write back: one wave per row, 16-B chunks along the row (coalesced)
-    const int lane = tid & 63, wave = tid >> 6, nwave = (nthr + 63) >> 6;
+    // (a block narrower than a wave -- wide rows leave 8-16 pixels per block --
+    // strides its lanes by the block width, not by 64)
+    const int lane = tid & 63, wave = tid >> 6, nwave = (nthr + 63) >> 6, lstep = nthr < 64 ? nthr : 64;
 #pragma unroll
     for (int kk = 0; kk < NP; ++kk) {
         const int n4 = a.wout[kk] >> 2;
         for (int r = wave; r < npix; r += nwave) {
             const f32x4 *src = reinterpret_cast<const f32x4 *>(lds + a.rowbase[kk] + r * a.S[kk]);
             f32x4 *dst = reinterpret_cast<f32x4 *>(a.g[kk] + (pblk + r) * a.ld[kk]);
-            for (int c4 = lane; c4 < n4; c4 += 64) {
+            for (int c4 = lane; c4 < n4; c4 += lstep) {
                 f32x4 v = src[c4];
                 if (a.accumulate) v += dst[c4];
                 dst[c4] = v;

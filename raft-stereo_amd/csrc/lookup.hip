@@ -773,6 +773,168 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// Cooperative span loads (dev variants 212-214 while measured).  The pair
+// kernel above has each lane fetch its own two spans with 7 (fp32) 16-B
+// loads: every wave-instruction then touches 64 different rows, and a span's
+// 128-B line is requested as two 64-B sectors by two different instructions.
+// Here LPS lanes load one span together (LPS x 16 B covers the span's
+// chunks), so one instruction covers 64 / LPS spans and asks for each line
+// once; the chunks land in LDS by buffer->LDS DMA (no VGPRs held while in
+// flight), and each pixel's lane reads its span back with NC ds_read_b128.
+// Same PairSpan fields and the same finish_pair, so the output is the pair
+// kernel's bit for bit.
+template <int R, bool BF16>
+struct CoopGeom {
+    typedef PairSpan<R, BF16> PS;
+    static constexpr int LPS = PS::NC <= 4 ? 4 : 8;   // lanes per span (16-B chunks)
+    static constexpr int SPI = 64 / LPS;              // spans per wave-instruction
+    static constexpr int NI = 64 / SPI;               // instructions per wave and level pair
+    static constexpr int SPAN_B = 64 * 16 * NI;       // LDS bytes per wave and level pair (1 KB per instr)
+    static_assert(PS::NC <= LPS, "span chunks exceed the lanes per span");
+    // chunk-position swizzle: lanes p and p + 8 of a ds_read_b128 lane group
+    // would hit the same banks with 8 lanes per span
+    __device__ static __forceinline__ int swz(int j) { return LPS == 8 ? (j & 1) : 0; }
+    // LDS byte offset of chunk c of the span of the wave's pixel p
+    __device__ static __forceinline__ int at(int p, int c) {
+        const int j = p / SPI;
+        return j * 1024 + ((c ^ swz(j)) * SPI + (p % SPI)) * 16;
+    }
+};
+
+// As issue_pair, but returns the span's byte offset (chunk 0) and the mask of
+// chunks to fetch instead of loading them.
+template <int R, bool BF16 = false>
+__device__ __forceinline__ uint32_t plan_pair(PairSpan<R, BF16> &ps, const LookupArgs &a, int lo, float x,
+                                              long long pblk, long long lrow) {
+    typedef PairSpan<R, BF16> PS;
+    const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+    const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+    ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));
+    ps.m = ps.inwin ? floorf(xhi) : 0.0f;
+    ps.n = ps.inwin ? floorf(xlo) : 0.0f;
+    const int dd = (int)ps.n - 2 * (int)ps.m;
+    ps.valid = ps.inwin && (dd == 0 || dd == 1);
+    int lo_e = 0x7FFFFFFF, hi_e = -1;
+    if (ps.inwin) {
+        int f, l;
+        tap_span<R>(xlo, Wlo, f, l);
+        if (f <= l) { lo_e = f; hi_e = l; }
+        tap_span<R>(xhi, Whi, f, l);
+        if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
+    }
+    const int sa = 2 * ((int)ps.m - R - 1);
+    const int ea = sa & ~(PS::EPC - 1);
+    ps.sh = sa - ea;
+    const long long ld = a.ld[lo];
+    const char *lvl = static_cast<const char *>(a.lvl[lo]);
+    const long long shb = a.shadow[lo];
+    uint32_t phase = 0;
+    if (shb != 0 && lo_e <= hi_e) {
+        const unsigned long long b0 =
+            (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + (lo_e & ~(PS::EPC - 1))) * PS::ES);
+        const unsigned long long b1 = (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + hi_e) * PS::ES);
+        const long long l0 = (long long)(b1 >> 7) - (long long)(b0 >> 7);
+        const long long l1 = (long long)((b1 + shb) >> 7) - (long long)((b0 + shb) >> 7);
+        phase = l1 < l0 ? 1u : 0u;
+    }
+    // the chunks [first, last] hold [lo_e, hi_e] (none: first > last)
+    int first = 7, last = 0;
+    if (lo_e <= hi_e) {
+        first = max((lo_e - ea) / PS::EPC, 0);
+        last = min((hi_e - ea) / PS::EPC, PS::NC - 1);
+    }
+    // packed plan: bits 0-22 the byte offset / 16 of chunk `first` (>= 0;
+    // lrow < 64, ld*ES <= 2^18: < 2^20), bit 23 shadow copy, bits 24-26 first
+    // chunk, 27-29 last chunk.  (Chunk 0 may start before the row: ea < 0.)
+    const uint32_t loc = first <= last ? (uint32_t)((lrow * ld + ea + PS::EPC * first) * PS::ES) >> 4 : 0u;
+    return loc | (phase << 23) | ((uint32_t)first << 24) | ((uint32_t)last << 27);
+}
+
+// One wave's cooperative fetch of the spans of level pair `lo` for its 64
+// pixels into `sbuf` (SPAN_B bytes): instruction j loads the spans of pixels
+// SPI*j .. SPI*j + SPI-1, lane l chunk (l / SPI) ^ swz(j) of pixel SPI*j + l % SPI.
+// Each pixel's plan travels in one dword (`pk`, see coop_pack): all the
+// wave's ds_bpermutes issue before its loads.
+template <int R, bool BF16>
+__device__ __forceinline__ void coop_fetch(const LookupArgs &a, int lo, long long pblk, uint32_t pk,
+                                           __attribute__((address_space(3))) char *sbuf) {
+    typedef CoopGeom<R, BF16> G;
+    typedef PairSpan<R, BF16> PS;
+    const int lane = threadIdx.x & 63;
+    const long long ld = a.ld[lo];
+    const uint32_t shb = (uint32_t)a.shadow[lo];
+    const auto rs = make_rsrc(static_cast<const char *>(a.lvl[lo]) + pblk * ld * PS::ES,
+                              clamp_bytes((a.P - pblk) * ld * PS::ES + a.shadow[lo]));
+    uint32_t v[G::NI];
+#pragma unroll
+    for (int j = 0; j < G::NI; ++j) v[j] = (uint32_t)__shfl((int)pk, G::SPI * j + lane % G::SPI, 64);
+#pragma unroll
+    for (int j = 0; j < G::NI; ++j) {
+        const int c = (lane / G::SPI) ^ G::swz(j);
+        const uint32_t first = (v[j] >> 24) & 7u, last = (v[j] >> 27) & 7u;
+        const uint32_t o = ((v[j] & 0x7FFFFFu) << 4) + ((v[j] >> 23) & 1u ? shb : 0u) + 16u * ((uint32_t)c - first);
+        const uint32_t off = ((uint32_t)c >= first && (uint32_t)c <= last) ? o : 0xFFFFFF00u;
+#if defined(__HIP_DEVICE_COMPILE__)   // the LDS-pointer builtin has no host form
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(sbuf + j * 1024),
+                                                 16, (int)off, 0, 0, 0);
+#else
+        (void)rs; (void)off;
+#endif
+    }
+}
+
+template <int R, bool BF16>
+__device__ __forceinline__ void coop_read(PairSpan<R, BF16> &ps, const char *sbuf) {
+    typedef CoopGeom<R, BF16> G;
+    const int p = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < PairSpan<R, BF16>::NC; ++k) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(sbuf + G::at(p, k));
+        ps.q[k][0] = v.x; ps.q[k][1] = v.y; ps.q[k][2] = v.z; ps.q[k][3] = v.w;
+    }
+}
+
+template <int R, int NL, int WPB, bool BF16 = false>
+__global__ __launch_bounds__(64 * WPB) void lookup_pair_coop_kernel(LookupArgs a) {
+    static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
+    typedef CoopGeom<R, BF16> G;
+    constexpr int NP = NL / 2;
+    __shared__ __attribute__((aligned(16))) char sbuf[WPB][NP][G::SPAN_B];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const long long pblk = (long long)blk * 64 * WPB;
+    const PairPixel q = pair_pixel<R, NL>(a, pblk);
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const long long pw = pblk + 64 * w;             // the wave's first pixel (wave-uniform)
+    PairSpan<R, BF16> sp[NP];
+    uint32_t pk[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) pk[k] = plan_pair<R, BF16>(sp[k], a, 2 * k, q.x, pw, q.pp - pw);
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        coop_fetch<R, BF16>(a, 2 * k, pw, pk[k], (__attribute__((address_space(3))) char *)sbuf[w][k]);
+    // both spans back into registers before any output store: a store is
+    // counted in vmcnt, so a later LDS read would wait for it too
+#pragma unroll
+    for (int k = 0; k < NP; ++k) coop_read<R, BF16>(sp[k], sbuf[w][k]);
+    auto sink = [&](int ch, float v) {
+        if (q.active) q.outp[(long long)ch * a.HW] = v;
+    };
+#pragma unroll
+    for (int k = 0; k < NP; ++k) finish_pair<R, false, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink);
+}
+
+template <int R, int WPB>
+static void launch_pair_coop(const LookupArgs &a, int bf16, hipStream_t s) {
+    const unsigned nblk = (unsigned)((a.P + 64 * WPB - 1) / (64 * WPB));
+    if (a.levels == 4) {
+        if (bf16) hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 4, WPB, true>), dim3(nblk), dim3(64 * WPB), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 4, WPB>), dim3(nblk), dim3(64 * WPB), 0, s, a);
+    } else {
+        if (bf16) hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 2, WPB, true>), dim3(nblk), dim3(64 * WPB), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 2, WPB>), dim3(nblk), dim3(64 * WPB), 0, s, a);
+    }
+}
+
 #ifdef RAFTCORR_DEV
 __device__ __forceinline__ unsigned long long rtc_stamp() {
     unsigned long long t;
@@ -827,6 +989,12 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
 #ifdef RAFTCORR_DEV
     if constexpr (R == 4) {
         const int v = dev_knob("RAFTCORR_LOOKUP_VARIANT");
+        if ((a.levels == 4 || a.levels == 2) && !a.out_cl && v >= 212 && v <= 214) {
+            if (v == 212) launch_pair_coop<R, 1>(a, bf16, s);
+            if (v == 213) launch_pair_coop<R, 2>(a, bf16, s);
+            if (v == 214) launch_pair_coop<R, 4>(a, bf16, s);
+            return hipGetLastError();
+        }
         if (a.levels == 4 && v == 210 && a.dbg) {
             hipLaunchKernelGGL((lookup_pair_stamped_kernel<R>), dim3(nblk), dim3(256), 0, s, a);
             return hipGetLastError();

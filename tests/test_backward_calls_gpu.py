@@ -77,7 +77,7 @@ def test_calls_vs_oracle_and_per_call(shape):
     calls_buf = rcorr.grad_buffers(P, widths, dev, pair=True, zero=False)
     for t in calls_buf:
         if t is not None:
-            (t.base if t.base is not None else t).fill_(float("nan"))
+            (t._base if t._base is not None else t).fill_(float("nan"))
     rcorr.lookup_backward_calls(calls_buf, cd, gd, L, r, overwrite=True)
     per_call = rcorr.grad_buffers(P, widths, dev, pair=True)
     for c, go in zip(cd, gd):
@@ -90,7 +90,7 @@ def test_calls_vs_oracle_and_per_call(shape):
         assert norm_err(got, want[k]) <= 1e-6 and rel_l2(got, want[k]) <= 1e-6, f"level {e} vs oracle"
         pc = per_call[e].cpu().numpy()
         assert norm_err(got, pc) <= 1e-6, f"level {e} vs per-call kernel"
-        full = calls_buf[e].base if calls_buf[e].base is not None else calls_buf[e]
+        full = calls_buf[e]._base if calls_buf[e]._base is not None else calls_buf[e]
         pad = full.view(P, -1)[:, widths[e]:].cpu().numpy()
         assert (pad == 0).all(), f"level {e}: padding not zeroed"
 
