@@ -256,8 +256,10 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
     dev = f1.device
     widths = [W2 >> i for i in range(L)]
     g = torch.Generator().manual_seed(99)
-    gouts = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(2)]
-    gl = [gouts[it % 2] for it in range(iters)]
+    # one output gradient per call, as in training (two alternating tensors
+    # would leave the calls' reads partly in the Infinity Cache)
+    gl = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(iters)]
+    gouts = gl
     pair = rcorr._pair_grads_ok(L, r, W2)      # the layout CorrBlock1D's autograd uses
     grads = rcorr.grad_buffers(P, widths, dev, pair=pair)
     cgrads = rcorr.grad_buffers(P, widths, dev, pair=pair, zero=False)
@@ -277,7 +279,7 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 4)]
         ev[0].record()
         for it in range(iters):
-            lbwd(coords[it], gouts[it % 2])
+            lbwd(coords[it], gl[it])
             ev[it + 1].record()
         rcorr.build_backward(f1, f2, grads)
         ev[iters + 1].record()
@@ -630,6 +632,13 @@ def main():
                else "rc::lookup_levelpar_kernel" if P < 65536 and L <= 4 else "rc::lookup_kernel")
     lname, lpmc = pmc_entry(pmc, lfamily)
     ltraffic = lpmc.get("hbm_bytes")
+    # FETCH_SIZE's scale depends on the access shape (profiles/r03/n/
+    # calib_scattered.txt): a wide stream reads 0.5x its bytes (hence the 2x
+    # of hbm_bytes), isolated 64-B / 128-B rows 2.0x / 1.0x their bytes, i.e.
+    # whole 128-B lines at 1x.  The lookup's reads are isolated lines, so the
+    # uncalibrated sum is the other end of the range its real traffic lies in.
+    ltraffic_raw = (lpmc["fetch_bytes_raw"] + lpmc["write_bytes_raw"]
+                    if "fetch_bytes_raw" in lpmc and "write_bytes_raw" in lpmc else None)
     roof_lookup = {"bound": "hbm", "achieved": lgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": lgbs / HBM_PEAK_GBS, "traffic": ltraffic,
                    "algorithmic_bytes": lbytes, "kernel": lname or lfamily,
@@ -638,6 +647,9 @@ def main():
         roof_lookup["traffic_gbs"] = ltraffic / (lookup_launch_ms * 1e-3) / 1e9
         roof_lookup["traffic_frac"] = roof_lookup["traffic_gbs"] / HBM_PEAK_GBS
         roof_lookup["traffic_over_algorithmic"] = ltraffic / lbytes
+    if ltraffic_raw:
+        roof_lookup["traffic_uncalibrated"] = ltraffic_raw
+        roof_lookup["traffic_uncalibrated_over_algorithmic"] = ltraffic_raw / lbytes
     if pmc:
         roof_lookup["pmc_source"] = f"{os.path.relpath(args.pmc, ROOT)} [{args.config}] {pmc.get('tag', '')}"
     dominant = roof_lookup if lookup_ms * iters >= build_ms else roof_volume
