@@ -12,7 +12,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Dev-only ablation flags (RAFTCORR_BUILD_MODE): 1 = no operand loads,
 // 2 = no epilogue stores.  Product launches use 0.
 enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8, kModeNoFragReads = 16,
-       kModeStagger = 64 };
+       kModeStagger = 64, kModeSched = 128, kModeReorder = 256,
+       kModeNoMfma = 512, kModeNoSplit = 1024 };
 
 // VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
 template <int VW>

@@ -90,6 +90,13 @@ __device__ __forceinline__ SplitFrag sp_read(const char *base) {
     float x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = *reinterpret_cast<const float *>(base + (j >> 1) * kSpBlk + (j & 1) * 512);
+    if constexpr (MODE & kModeNoSplit) {     // dev timing probe: head piece only, reused thrice
+        u32x4s h;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = sp_pack(x[2 * k], x[2 * k + 1]);
+        const bf16x8 hb = __builtin_bit_cast(bf16x8, h);
+        return SplitFrag{hb, hb, hb};
+    }
     return sp_split(x);
 }
 
@@ -157,21 +164,63 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
             const char *st = smem + ((2 * ks + (g >> 1)) % kSpSL) * kSpSlot + lrow;
             const char *pb = st + 4 * (c.o1 + i);                        // F1 (B): this wave's w1
             const char *pa = st + kSpOp + 4 * (c.o2 + i);                // F2 (A): this wave's w2
+            // small terms first (the six leading products of h+m+l)
+            auto mma6 = [&](f32x4 &c, const SplitFrag &x, const SplitFrag &y) {
+                if constexpr (MODE & kModeNoMfma) {   // dev timing probe: keep the split live
+                    const u32x4s a = __builtin_bit_cast(u32x4s, x.h) ^ __builtin_bit_cast(u32x4s, x.m) ^
+                                     __builtin_bit_cast(u32x4s, x.l) ^ __builtin_bit_cast(u32x4s, y.h) ^
+                                     __builtin_bit_cast(u32x4s, y.m) ^ __builtin_bit_cast(u32x4s, y.l);
+                    c[0] += __builtin_bit_cast(float, a[0] | a[1] | a[2] | a[3]);
+                    return;
+                }
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.m, y.m, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.l, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.l, y.h, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.m, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.m, y.h, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.h, c, 0, 0, 0);
+            };
             SplitFrag fb[FB];
-#pragma unroll
-            for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE>(pb + 64 * n);
-#pragma unroll
-            for (int m = 0; m < FA; ++m) {
-                const SplitFrag fa = sp_read<MODE>(pa + 64 * m);
+            if constexpr (MODE & (kModeSched | kModeReorder)) {
+                // pipelined order (dev A/B): only A0 and B0 are split before
+                // the first MFMA; B1.. are split while the MFMAs of A0 run,
+                // A(m+1) while those of A(m) run.  Same products, same
+                // order per accumulator: bit-identical.
+                SplitFrag fa = sp_read<MODE>(pa);
+                fb[0] = sp_read<MODE>(pb);
 #pragma unroll
                 for (int n = 0; n < FB; ++n) {
-                    // small terms first (the six leading products of h+m+l)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.m, fb[n].m, acc[m][n], 0, 0, 0);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.h, fb[n].l, acc[m][n], 0, 0, 0);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.l, fb[n].h, acc[m][n], 0, 0, 0);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.h, fb[n].m, acc[m][n], 0, 0, 0);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.m, fb[n].h, acc[m][n], 0, 0, 0);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.h, fb[n].h, acc[m][n], 0, 0, 0);
+                    if (n + 1 < FB) fb[n + 1] = sp_read<MODE>(pb + 64 * (n + 1));
+                    mma6(acc[0][n], fa, fb[n]);
+                }
+#pragma unroll
+                for (int m = 1; m < FA; ++m) {
+                    fa = sp_read<MODE>(pa + 64 * m);
+#pragma unroll
+                    for (int n = 0; n < FB; ++n) mma6(acc[m][n], fa, fb[n]);
+                }
+                if constexpr (MODE & kModeSched) {
+                    // the schedule: A0 + B0 up front (8 LDS reads, their split),
+                    // then one MFMA per ~3 VALU with an LDS read every 4th
+                    constexpr int NM = 6 * FA * FB, NV = 36 * (FA + FB - 2) + 8;
+                    constexpr int VPM = (NV + NM - 1) / NM;
+                    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 72, 0);
+#pragma unroll
+                    for (int k = 0; k < NM; ++k) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+                        if (k % 4 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE>(pb + 64 * n);
+#pragma unroll
+                for (int m = 0; m < FA; ++m) {
+                    const SplitFrag fa = sp_read<MODE>(pa + 64 * m);
+#pragma unroll
+                    for (int n = 0; n < FB; ++n) mma6(acc[m][n], fa, fb[n]);
                 }
             }
         }
@@ -556,6 +605,12 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         case 4: hipLaunchKernelGGL((rc::build_split_kernel<4, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 6: hipLaunchKernelGGL((rc::build_split_kernel<6, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 7: hipLaunchKernelGGL((rc::build_split_kernel<7, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 128: hipLaunchKernelGGL((rc::build_split_kernel<128, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 512: hipLaunchKernelGGL((rc::build_split_kernel<512, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 1024: hipLaunchKernelGGL((rc::build_split_kernel<1024, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 1027: hipLaunchKernelGGL((rc::build_split_kernel<1027, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 515: hipLaunchKernelGGL((rc::build_split_kernel<515, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 256: hipLaunchKernelGGL((rc::build_split_kernel<256, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         default: break;
     }
 #endif
