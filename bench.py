@@ -331,10 +331,16 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
            "volume_bwd_us": vb_ms * 1e3,
            "train_step_ms": step_ms, "train_pairs_per_s": B / (step_ms * 1e-3),
            "train_step_per_call_bwd_ms": step_per_call_ms,
+           # split-bf16 GEMMs (the default since ABI v8): 6 bf16 MFMA products per
+           # fp32 product; priced as fp32-equivalent FLOP/s against the fp32
+           # MFMA peak (as roofline_volume) and as executed bf16 FLOP/s
            "roofline_volume_bwd": {"bound": "mfma", "achieved": vflops / (vb_ms * 1e-3) / 1e12,
                                    "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                    "frac": vflops / (vb_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                                   "kernel": ("rc::volume_bwd_kernel<true,kPairFold>" if pair
+                                   "mfma_bf16_executed_tflops": 6 * vflops / (vb_ms * 1e-3) / 1e12,
+                                   "mfma_bf16_frac": 6 * vflops / (vb_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS,
+                                   "kernel": ("rc::volume_bwd_split_kernel<true,kPairFold>" if pair
+                                              else "rc::volume_bwd_split_kernel<true,1>" if L == 2
                                               else f"rc::volume_bwd_kernel<true,{L}>")},
            "roofline_lookup_bwd_per_call": {
                "bound": "hbm", "achieved": lbytes / (lb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -704,7 +710,7 @@ def main():
                 rl["traffic_frac"] = rl["traffic_gbs"] / HBM_PEAK_GBS
                 rl["traffic_over_algorithmic"] = rl["traffic"] / rl["algorithmic_bytes"]
         rv = result["backward"]["roofline_volume_bwd"]
-        vbname, vbpmc = pmc_entry(pmc, "rc::volume_bwd_kernel")
+        vbname, vbpmc = pmc_entry(pmc, rv["kernel"].split("<")[0])
         if "mfma_util" in vbpmc:    # the exact instance the backward ran (one per config)
             rv["kernel"] = vbname
             rv["mfma_util_pmc"] = vbpmc["mfma_util"]

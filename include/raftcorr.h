@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 7
+#define RC_ABI_VERSION 8
 
 /* element types */
 #define RC_F32  0
@@ -238,9 +238,15 @@ int rc_corr_lookup_backward_calls(void *const *grad_pyr, const int *widths, cons
  *   (avg_pool2d's backward, floor widths), G = Dl_0 / sqrtf(D), and
  *   grad_fmap1[b][d][h][w1] = sum_w2 G[b,h,w1,w2] * fmap2[b][d][h][w2]
  *   grad_fmap2[b][d][h][w2] = sum_w1 G[b,h,w1,w2] * fmap1[b][d][h][w1]
- *   (overwritten, fp32, exact-fp32 MFMA).  grad_pyr[l], l < levels: fp32
- *   B*H*W1 rows of W2 >> l, row stride grad_ld[l] (grad_ld[0] % 4 == 0).
- *   fmap_dtype RC_F32 only.  When B*H*W1 == 0 nothing is written.
+ *   (overwritten, fp32).  grad_pyr[l], l < levels: fp32 B*H*W1 rows of
+ *   W2 >> l, row stride grad_ld[l] (grad_ld[0] % 4 == 0).  fmap_dtype RC_F32
+ *   only.  When B*H*W1 == 0 nothing is written.
+ *   ABI v8: the two GEMMs run on bf16 MFMA with every fp32 operand split
+ *   exactly into three bf16 pieces (six products per fp32 product, fp32
+ *   accuracy, as rc_corr_build's default) when W1 % 4 == W2 % 4 == 0 and the
+ *   gradients are pair-folded or 1-2 levels; otherwise, or with
+ *   fmap_dtype | RC_BUILD_EXACT_F32 (needed only for non-finite values), on
+ *   exact fp32 MFMA.
  *   levels == 3 with grad_pyr[1] == NULL: pair-folded gradients from
  *   rc_corr_lookup_backward's pair layout, Dl_0[k] = g_0[k] + g_2[k>>2] / 4;
  *   with levels | RC_SHADOW_LEVEL(0) / (2) each g_l is primary + shadow copy. */

@@ -17,7 +17,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 RC_F32, RC_BF16 = 0, 1
 RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
-ABI_VERSION = 7
+ABI_VERSION = 8
 RC_SHADOW = 0xFF00  # pyr_dtype flags: every stored level carries a line-phase shadow copy
 RC_OUT_CHANNELS_LAST = 0x10000   # pyr_dtype flag: NHWC lookup output (pair kernel)
 RC_BUILD_EXACT_F32 = 0x20000     # rc_corr_build flag: exact fp32 MFMA kernel instead of the split-bf16 one

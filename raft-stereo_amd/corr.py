@@ -458,10 +458,11 @@ def lookup_backward_calls(grads, coords_list, grad_out_list, num_levels, radius,
     _lib.check(rc, "rc_corr_lookup_backward_calls")
 
 
-def build_backward(fmap1, fmap2, grads):
+def build_backward(fmap1, fmap2, grads, exact_f32=False):
     """rc_corr_build_backward: level gradients -> (d fmap1, d fmap2), fp32.
     The pooling backward (model.py:294), the 1/sqrt(D) (:326) and the two
-    einsum operand gradients (:324) in one launch."""
+    einsum operand gradients (:324) in one launch -- on split-bf16 MFMA
+    (fp32 accuracy) by default, on exact fp32 MFMA with ``exact_f32``."""
     f1 = fmap1.detach().float().contiguous()
     f2 = fmap2.detach().float().contiguous()
     B, D, H, W1 = f1.shape
@@ -475,7 +476,8 @@ def build_backward(fmap1, fmap2, grads):
         grads = [grads[0], None, grads[2]] if len(grads) > 2 else [grads[0]]
     with torch.cuda.device(f1.device):
         rc = _lib.lib().rc_corr_build_backward(
-            f1.data_ptr(), f2.data_ptr(), _lib.RC_F32, B, D, H, W1, W2,
+            f1.data_ptr(), f2.data_ptr(), _lib.RC_F32 | (_lib.RC_BUILD_EXACT_F32 if exact_f32 else 0),
+            B, D, H, W1, W2,
             _lib.ptr_array([None if g is None else g.data_ptr() for g in grads]),
             _lib.long_array([W2 >> l if g is None else g.stride(0) for l, g in enumerate(grads)]),
             len(grads) | flags, df1.data_ptr(), df2.data_ptr(), _stream(f1.device))
@@ -530,8 +532,10 @@ class _GradState:
     buffers it never zeroes.  Otherwise each lookup node adds its call into
     zeroed buffers right away (rc_corr_lookup_backward)."""
 
-    def __init__(self, P, widths, device, num_levels, radius, grad_shadow=None, deferred=None):
+    def __init__(self, P, widths, device, num_levels, radius, grad_shadow=None, deferred=None,
+                 exact_f32=False):
         self.P, self.widths, self.device = P, widths, device
+        self.exact_f32 = bool(exact_f32)
         self.num_levels, self.radius = num_levels, radius
         self.pair = _pair_grads_ok(num_levels, radius, widths[0])
         if grad_shadow is None:
@@ -588,7 +592,7 @@ class _BuildFn(torch.autograd.Function):
         grads = ctx.state.take()
         if grads is None:          # no lookup output reached the loss
             return None, None, None
-        df1, df2 = build_backward(f1, f2, grads)
+        df1, df2 = build_backward(f1, f2, grads, exact_f32=ctx.state.exact_f32)
         return df1.to(f1.dtype), df2.to(f2.dtype), None
 
 
@@ -690,7 +694,7 @@ class CorrBlock1D:
         if grad:
             self._state = _GradState(B * H * W1, [W2 >> i for i in range(num_levels)],
                                      fmap1.device, num_levels, radius, grad_shadow,
-                                     deferred=grad_deferred)
+                                     deferred=grad_deferred, exact_f32=exact_f32)
             self._token = _BuildFn.apply(fmap1, fmap2, self._state)
 
     @property

@@ -35,6 +35,7 @@
 //     output stores.  The workgroups of one (b,h) row are remapped onto one
 //     XCD, which then reads that row's operands from HBM once.
 #include "common.h"
+#include "split.h"
 
 namespace rc {
 
@@ -722,6 +723,134 @@ void volume_bwd_kernel(BuildBwdArgs a, int nwg_total) {
     }
 }
 
+// volume_bwd_split_kernel -- the same two GEMMs on bf16 MFMA by the exact
+// three-way split of every fp32 operand (split.h; the forward's arithmetic,
+// DESIGN.md §3.1c, §3.4): per 32-k step six v_mfma_f32_16x16x32_bf16 per
+// 16x16 output fragment pair instead of eight v_mfma_f32_16x16x4f32.
+// Staging, fold and output stores are volume_bwd_kernel's with 32-k stages
+// (LDS rows of 40 floats, 80 KiB: two workgroups per CU).  A lane (i16, g)
+// supplies k = 4g..4g+3 and 16+4g..16+4g+3 of its row to the MFMA's 8-k
+// slot g (the sum over k is order-free; both operands use the same
+// permutation), i.e. two conflict-free ds_read_b128 at row*40 + 4g and +16.
+template <bool VEC, int NLEV>
+__global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a, int nwg_total) {
+    static_assert(NLEV >= kPairFold, "level count");
+    typedef BwdTile<32> TL;
+    constexpr int kBwdK = 32, kBwdRow = TL::ROW, QPT = TL::QPT;
+    __shared__ __attribute__((aligned(16))) float smem[2][2][TL::IMG];   // [buf][X | Y]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wgid = xcd_remap(blockIdx.x, nwg_total);   // one (b,h) row's tiles on one XCD
+    const int T1 = a.tm * a.tn1, T = T1 + a.tm * a.tn2;
+    const int row = wgid / T;
+    int tile = wgid - row * T;
+    const bool kind2 = tile >= T1;              // false: a dF1 tile, true: a dF2 tile
+    if (kind2) tile -= T1;
+    const int tn = kind2 ? a.tn2 : a.tn1;
+    const int tmi = tile / tn, tni = tile - tmi * tn;
+    const int b = row / a.H, h = row - b * a.H;
+    const int D = a.D, H = a.H, W1 = a.W1;
+    const int K = kind2 ? W1 : a.W2;            // reduction length
+    const int N = kind2 ? a.W2 : W1;            // output row length
+    const int m0 = tmi * 128, n0 = tni * 128;
+    const long long prow0 = (long long)row * W1;
+    const float *X = kind2 ? a.f1 : a.f2;
+    float *out = kind2 ? a.df2 : a.df1;
+
+    constexpr int QR = kBwdK / 4;
+    f32x4 rx[QPT];
+    FoldRaw<NLEV> ry[QPT];
+    auto load_stage = [&](int kb) {
+#pragma unroll
+        for (int u = 0; u < QPT; ++u) {
+            const int c = tid + 256 * u;
+            const int r = c / QR, kq = 4 * (c % QR);
+            const int d = m0 + r;
+            const float *xrow = X + ((long long)(b * D + (d < D ? d : 0)) * H + h) * K;
+            rx[u] = load_x_quad<VEC>(xrow, kb + kq, K, d < D);
+            if (!kind2) {
+                const int w1 = n0 + r;
+                fold_load<NLEV>(a, prow0 + w1, kb + kq, w1 < W1, ry[u]);
+            } else {
+                const int w1 = kb + (c % kBwdK);
+                fold_load<NLEV>(a, prow0 + w1, n0 + 4 * (c / kBwdK), w1 < W1, ry[u]);
+            }
+        }
+    };
+    auto write_stage = [&](int buf, int kb) {
+        float *sx = smem[buf][0], *sy = smem[buf][1];
+#pragma unroll
+        for (int u = 0; u < QPT; ++u) {
+            const int c = tid + 256 * u;
+            const int r = c / QR, kq = 4 * (c % QR);
+            *reinterpret_cast<f32x4 *>(sx + r * kBwdRow + kq) = rx[u];
+            if (!kind2) {
+                *reinterpret_cast<f32x4 *>(sy + r * kBwdRow + kq) = fold_math<NLEV>(a, kb + kq, ry[u]);
+            } else {
+                const int k = c % kBwdK, nq = 4 * (c / kBwdK);
+                const f32x4 gq = fold_math<NLEV>(a, n0 + nq, ry[u]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sy[(nq + e) * kBwdRow + k] = gq[e];
+            }
+        }
+    };
+    // a lane's fragment of image row `rr`: k = 4g..4g+3 and 16+4g..16+4g+3
+    auto frag = [&](const float *img, int rr, int g) {
+        const f32x4 lo = *reinterpret_cast<const f32x4 *>(img + rr * kBwdRow + 4 * g);
+        const f32x4 hi = *reinterpret_cast<const f32x4 *>(img + rr * kBwdRow + 16 + 4 * g);
+        const float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return sp_split(x);
+    };
+
+    // wave tile: 64 d (X rows) x 64 n (Y rows); acc[nb][ma] = out^T fragment
+    const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+    const int g = lane >> 4, i16 = lane & 15;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nst = (K + kBwdK - 1) / kBwdK;
+    load_stage(0);
+    write_stage(0, 0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nst) load_stage((st + 1) * kBwdK);
+        const float *sx = smem[buf][0], *sy = smem[buf][1];
+        SplitFrag bx[4];
+#pragma unroll
+        for (int ma = 0; ma < 4; ++ma) bx[ma] = frag(sx, wm + 16 * ma + i16, g);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+            const SplitFrag ay = frag(sy, wn + 16 * nb + i16, g);
+#pragma unroll
+            for (int ma = 0; ma < 4; ++ma) sp_mma6(acc[nb][ma], ay, bx[ma]);
+        }
+        if (st + 1 < nst) write_stage(buf ^ 1, (st + 1) * kBwdK);
+        __syncthreads();
+    }
+
+    // lane holds out^T[n = 4g + r][d = i16] of fragment (nb, ma): 4 consecutive n
+#pragma unroll
+    for (int ma = 0; ma < 4; ++ma) {
+        const int d = m0 + wm + 16 * ma + i16;
+        if (d >= D) continue;
+        float *orow = out + ((long long)(b * D + d) * H + h) * N;
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+            const int n = n0 + wn + 16 * nb + 4 * g;
+            if (VEC && n + 3 < N) {
+                *reinterpret_cast<f32x4 *>(orow + n) = acc[nb][ma];
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (n + r < N) orow[n + r] = acc[nb][ma][r];
+            }
+        }
+    }
+}
+
 }  // namespace rc
 
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s) {
@@ -807,6 +936,19 @@ hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s) {
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     const bool vec = (a.W1 % 4 == 0) && (a.W2 % 4 == 0);
     const dim3 grid((unsigned)nwg), blk(256);
+    // the split-bf16 kernel (fp32 accuracy on bf16 MFMA) unless the exact
+    // fp32 MFMA kernel is asked for (RC_BUILD_EXACT_F32, non-finite inputs)
+    // (the split kernel is instantiated where it fits 256 VGPRs without
+    // spilling: vector rows (widths % 4 == 0) and the pair-folded, 1- and
+    // 2-level gradients; 3+ per-level layouts and odd widths keep the exact
+    // kernel)
+    const bool pairfold = a.nlev == 3 && a.g[1] == nullptr;
+    if (!a.exact && vec && (pairfold || a.nlev == 1 || a.nlev == 2)) {
+        if (pairfold) hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, rc::kPairFold>), grid, blk, 0, s, a, (int)nwg);
+        else if (a.nlev == 1) hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, 1>), grid, blk, 0, s, a, (int)nwg);
+        else hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, 2>), grid, blk, 0, s, a, (int)nwg);
+        return hipGetLastError();
+    }
     // 16-k stages for every level count: 49 KB of LDS lets three workgroups
     // share a CU (round 1 staged 32 for 1-2 levels: 851 / 976 us vs 718 /
     // 862 us at config 2 with 1 / 2 levels, the same bits)

@@ -516,6 +516,8 @@ extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int 
     if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
         return fail(RC_EINVAL, "rc_corr_build_backward: bad shape B=%d D=%d H=%d W1=%d W2=%d", B, D,
                     H, W1, W2);
+    const bool exact_f32 = (fmap_dtype & RC_BUILD_EXACT_F32) != 0;
+    fmap_dtype &= ~RC_BUILD_EXACT_F32;
     if (fmap_dtype != RC_F32)
         return fail(RC_EUNSUPPORTED, "rc_corr_build_backward: fp32 feature maps only");
     if (levels < 1 || levels > RC_MAX_LEVELS || (W2 >> (levels - 1)) < 1)
@@ -555,6 +557,7 @@ extern "C" int rc_corr_build_backward(const void *fmap1, const void *fmap2, int 
         return fail(RC_EINVAL, "rc_corr_build_backward: level-0 row stride %lld is not a multiple "
                     "of 4", a.ld[0]);
     a.nlev = levels;
+    a.exact = exact_f32 ? 1 : 0;
     a.f1 = static_cast<const float *>(fmap1);
     a.f2 = static_cast<const float *>(fmap2);
     a.df1 = grad_fmap1;

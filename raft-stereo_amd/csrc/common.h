@@ -178,6 +178,7 @@ struct BuildBwdArgs {
     float scale, sq;
     int pow2;
     long long shadow[kMaxLevels];   // floats from g[l] to its RC_SHADOW copy (kPairFold), 0 = none
+    int exact;                      // 1: exact fp32 MFMA kernel (RC_BUILD_EXACT_F32); 0: split-bf16
 };
 
 }  // namespace rc

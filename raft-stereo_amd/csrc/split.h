@@ -1,0 +1,54 @@
+// The exact three-way bf16 split of fp32 operands shared by the split-bf16
+// MFMA kernels (volume_split.hip: the forward volume; backward.hip: the
+// volume backward): x = h + m + l exactly for finite |x| < 3.39e38, and the
+// six leading products of (h+m+l)(h'+m'+l') on v_mfma_f32_16x16x32_bf16
+// (DESIGN.md §3.1c).
+#pragma once
+#include "common.h"
+#include "epilogue.h"
+
+namespace rc {
+
+typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+typedef __bf16 sp_bf16x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> packed bf16 (RNE), and back to fp32
+__device__ __forceinline__ uint32_t sp_pack(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, sp_bf16x2));   // v_cvt_pk_bf16_f32
+}
+__device__ __forceinline__ float sp_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float sp_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xFFFF0000u); }
+
+struct SplitFrag {
+    bf16x8 h, m, l;
+};
+
+// 8 consecutive d of one w -> head, middle and low bf16 pieces (each exact
+// residual of the previous: x = h + m + l for finite |x| < 3.39e38).
+__device__ __forceinline__ SplitFrag sp_split(const float (&x)[8]) {
+    u32x4s h, m, l;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t hp = sp_pack(x[2 * k], x[2 * k + 1]);
+        const float r0 = x[2 * k] - sp_lo(hp), r1 = x[2 * k + 1] - sp_hi(hp);      // exact
+        const uint32_t mp = sp_pack(r0, r1);
+        const float s0 = r0 - sp_lo(mp), s1 = r1 - sp_hi(mp);                      // exact
+        h[k] = hp;
+        m[k] = mp;
+        l[k] = sp_pack(s0, s1);
+    }
+    return SplitFrag{__builtin_bit_cast(bf16x8, h), __builtin_bit_cast(bf16x8, m), __builtin_bit_cast(bf16x8, l)};
+}
+
+// c += a * b to fp32 accuracy: the six leading piece products, small terms
+// first (mm + hl + lh + hm + mh + hh); ml, lm, ll (< 2^-27 |a||b|) dropped.
+__device__ __forceinline__ void sp_mma6(f32x4 &c, const SplitFrag &x, const SplitFrag &y) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.m, y.m, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.l, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.l, y.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.m, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.m, y.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.h, c, 0, 0, 0);
+}
+
+}  // namespace rc

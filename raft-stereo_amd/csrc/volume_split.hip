@@ -39,6 +39,7 @@
 // skipped (template FA / FB), so W = 240 wastes no MFMA work.
 #include "common.h"
 #include "epilogue.h"
+#include "split.h"
 
 namespace rc {
 
@@ -50,37 +51,6 @@ constexpr int kSpSL = 4;                    // ring slots (stages): one K step i
 constexpr int kSpMaxFused = 5;              // levels the epilogue writes (more: pooled from memory)
 constexpr int kSpStb = 16 * (64 + 4) * 4;   // per-wave epilogue staging (epilogue_swapped, WT 64)
 static_assert(4 * kSpStb <= kSpSL * kSpSlot, "epilogue staging aliases the ring");
-
-typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
-typedef __bf16 sp_bf16x2 __attribute__((ext_vector_type(2)));
-
-// two fp32 -> packed bf16 (RNE), and back to fp32
-__device__ __forceinline__ uint32_t sp_pack(float lo, float hi) {
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, sp_bf16x2));   // v_cvt_pk_bf16_f32
-}
-__device__ __forceinline__ float sp_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
-__device__ __forceinline__ float sp_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xFFFF0000u); }
-
-struct SplitFrag {
-    bf16x8 h, m, l;
-};
-
-// 8 consecutive d of one w -> head, middle and low bf16 pieces (each exact
-// residual of the previous: x = h + m + l for finite |x| < 3.39e38).
-__device__ __forceinline__ SplitFrag sp_split(const float (&x)[8]) {
-    u32x4s h, m, l;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t hp = sp_pack(x[2 * k], x[2 * k + 1]);
-        const float r0 = x[2 * k] - sp_lo(hp), r1 = x[2 * k + 1] - sp_hi(hp);      // exact
-        const uint32_t mp = sp_pack(r0, r1);
-        const float s0 = r0 - sp_lo(mp), s1 = r1 - sp_hi(mp);                      // exact
-        h[k] = hp;
-        m[k] = mp;
-        l[k] = sp_pack(s0, s1);
-    }
-    return SplitFrag{__builtin_bit_cast(bf16x8, h), __builtin_bit_cast(bf16x8, m), __builtin_bit_cast(bf16x8, l)};
-}
 
 // One lane's fragment: rows r0..r0+7 (d inside the stage) of w column w of an
 // operand tile at LDS byte address base.  Row d of the tile sits in block
@@ -164,7 +134,6 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
             const char *st = smem + ((2 * ks + (g >> 1)) % kSpSL) * kSpSlot + lrow;
             const char *pb = st + 4 * (c.o1 + i);                        // F1 (B): this wave's w1
             const char *pa = st + kSpOp + 4 * (c.o2 + i);                // F2 (A): this wave's w2
-            // small terms first (the six leading products of h+m+l)
             auto mma6 = [&](f32x4 &c, const SplitFrag &x, const SplitFrag &y) {
                 if constexpr (MODE & kModeNoMfma) {   // dev timing probe: keep the split live
                     const u32x4s a = __builtin_bit_cast(u32x4s, x.h) ^ __builtin_bit_cast(u32x4s, x.m) ^
@@ -173,12 +142,7 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
                     c[0] += __builtin_bit_cast(float, a[0] | a[1] | a[2] | a[3]);
                     return;
                 }
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.m, y.m, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.l, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.l, y.h, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.m, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.m, y.h, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.h, c, 0, 0, 0);
+                sp_mma6(c, x, y);
             };
             SplitFrag fb[FB];
             if constexpr (MODE & (kModeSched | kModeReorder)) {

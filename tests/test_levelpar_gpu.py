@@ -3,6 +3,7 @@ gives each level its own wave below 64K pixels (lookup_levelpar_kernel).
 Same values bit for bit as the default block (pair / chain kernels), incl.
 NaN/inf/subnormal coords and the fused loop step updating coords in place
 (the kernel's block barrier orders the coords reads before the writes)."""
+import numpy as np
 import pytest
 import torch
 
@@ -36,3 +37,35 @@ def test_low_latency_bit_identical(shape, dt):
         for u, v in zip(a, b):
             assert torch.equal(u.view(torch.int32), v.view(torch.int32))
         assert torch.equal(c_ref.view(torch.int32), c_ll.view(torch.int32))
+
+
+# below 64K pixels every rc_corr_lookup with 1-4 levels takes the
+# level-parallel kernel, whatever the radius (1-8); shapes the chain / pair
+# kernels never served (1 level, radius > 4) against the C oracle, bit for bit.
+LEVELPAR_EXTRA = [
+    # B, D, H, W1, W2, L, r
+    (1, 16, 2, 40, 48, 1, 3),
+    (1, 16, 2, 33, 64, 1, 8),
+    (2, 8, 2, 30, 64, 2, 6),
+    (1, 16, 3, 45, 90, 3, 5),
+    (1, 8, 2, 50, 128, 4, 7),
+]
+
+
+@pytest.mark.parametrize("shape", LEVELPAR_EXTRA, ids=lambda s: "x".join(map(str, s)))
+def test_levelpar_levels_radius_vs_oracle(shape):
+    from oracle import coracle
+    from raft_stereo_amd import corr as rcorr
+    B, D, H, W1, W2, L, r = shape
+    g = torch.Generator().manual_seed(sum(shape) + 99)
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    c = special_coords(B, H, W1, W2, g)
+    with torch.no_grad():
+        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=True)
+        pyr = [t.reshape(t.shape[0], -1) for t in blk.corr_pyramid[:L]]
+        a = blk(c.to(DEV)).cpu().numpy()
+        b = rcorr.lookup(blk.corr_pyramid, c.to(DEV), L, r).cpu().numpy()
+    ref = coracle.corr_lookup([t.cpu().numpy() for t in pyr], c.numpy(), L, r)
+    assert np.array_equal(a, ref, equal_nan=True)
+    assert np.array_equal(b, ref, equal_nan=True)
