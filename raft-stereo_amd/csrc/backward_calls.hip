@@ -154,8 +154,136 @@ __device__ __forceinline__ void bwd_call_add(const BwdCall<R> &c, float *row, co
     }
 }
 
+// ---- software-pipelined form (the product since r03) ----------------------
+// The same sums, bit for bit, with two changes to the lane's chain:
+//  * one read-modify-write per call: both strips lie inside the 2NJ-element
+//    window [2(m-R), 2(m+R+2)) of level 2k (n = 2m + dd), so the window is
+//    read once, gets the level-(2k+1) pair contributions and then the
+//    level-2k ones in registers (each element: + pair value, then + own
+//    value, as the two separate updates did -- extra +0.0 adds are
+//    identities, a row never holds -0.0), and is written once;
+//  * the window's reads issue before the NEXT call's tap math, which then
+//    hides their latency.
+template <int R>
+struct CallStrip {
+    static constexpr int NJ = 2 * R + 2;
+    float s0[NJ], s1[NJ];
+    int m, dd;
+    bool live, fast;
+};
+
+template <int R>
+__device__ __forceinline__ void strip_compute(CallStrip<R> &s, const BwdCall<R> &c, const PairGeom &g) {
+    constexpr int T = 2 * R + 1, NJ = 2 * R + 2;
+    const float xlo = c.x * g.slo, xhi = c.x * g.shi;
+    const bool inw = xhi > -(float)(R + 4) && xhi < (float)(g.Whi + R + 4);   // false for NaN
+    const float mf = inw ? floorf(xhi) : 0.0f, nf = inw ? floorf(xlo) : 0.0f;
+    s.m = (int)mf;
+    const int n = (int)nf;
+    s.live = inw && s.m >= -R - 2 && s.m <= g.Whi + R;
+    s.dd = n - 2 * s.m;
+    bool fast = s.dd == 0 || s.dd == 1;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s.s0[j] = s.s1[j] = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xp = e ? tap_pos(xhi, t - R, g.dvhi, g.halfhi) : tap_pos(xlo, t - R, g.dvlo, g.halflo);
+            const float x0 = floorf(xp);
+            const float gv = c.gv[e][t];
+            const float c1 = (xp - x0) * gv, c0 = ((x0 + 1.0f) - xp) * gv;
+            fast = fast && (x0 == (e ? mf : nf) + (float)(t - R));
+            if (e == 0) {
+                s.s0[t] += c0;
+                s.s0[t + 1] += c1;
+            } else {
+                s.s1[t] += c0 * 0.5f;
+                s.s1[t + 1] += c1 * 0.5f;
+            }
+        }
+    }
+    s.fast = fast;
+}
+
+// Apply call `cur` (its window read already issued into w) and compute the
+// strips of the next call in between.
+template <int R>
+__device__ __forceinline__ void strip_apply_fast(const CallStrip<R> &s, f32x2 (&w)[2 * R + 2], float *row,
+                                                 const PairGeom &g) {
+    constexpr int NJ = 2 * R + 2;
+    const int jb = s.m - R, ib = 2 * s.m + s.dd - R;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {                  // level 2k+1: c/2 to both children
+        const float v = (jb + j >= 0 && jb + j < g.Whi) ? s.s1[j] : 0.0f;
+        w[j][0] += v;
+        w[j][1] += v;
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * NJ; ++k) {              // level 2k: window element k = dd + R + j
+        const int j0 = k - R, j1 = k - R - 1;
+        const float v0 = (j0 >= 0 && j0 < NJ && ib + j0 >= 0 && ib + j0 < g.Wlo) ? s.s0[j0 < 0 ? 0 : (j0 >= NJ ? NJ - 1 : j0)] : 0.0f;
+        const float v1 = (j1 >= 0 && j1 < NJ && ib + j1 >= 0 && ib + j1 < g.Wlo) ? s.s0[j1 < 0 ? 0 : (j1 >= NJ ? NJ - 1 : j1)] : 0.0f;
+        w[k >> 1][k & 1] += s.dd ? v1 : v0;
+    }
+    f32x2 *q = reinterpret_cast<f32x2 *>(row + 2 * (s.m - R));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) q[j] = w[j];
+}
+
+template <int R>
+__device__ __forceinline__ void strip_apply_slow(const CallStrip<R> &s, const BwdCall<R> &c, float *row,
+                                                 const PairGeom &g) {
+    constexpr int T = 2 * R + 1;
+    const float xlo = c.x * g.slo, xhi = c.x * g.shi;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int W = e ? g.Whi : g.Wlo;
+        const float Wm1 = (float)(W - 1);
+        for (int t = 0; t < T; ++t) {
+            const float xp = e ? tap_pos(xhi, t - R, g.dvhi, g.halfhi) : tap_pos(xlo, t - R, g.dvlo, g.halflo);
+            const float x0 = floorf(xp);
+            const float gv = c.gv[e][t];
+            const float c1 = (xp - x0) * gv, c0 = ((x0 + 1.0f) - xp) * gv;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float xe = x0 + (float)q;
+                if (!(xe >= 0.0f && xe <= Wm1)) continue;
+                const float cc = q ? c1 : c0;
+                const int k = (int)xe;
+                if (e == 0) {
+                    row[k] += cc;
+                } else {
+                    row[2 * k] += cc * 0.5f;
+                    row[2 * k + 1] += cc * 0.5f;
+                }
+            }
+        }
+    }
+}
+
+// one pipeline step: apply `cur` (call c, when `valid`), compute `cur` anew
+// from `nb` (call c + 1) while its window reads are in flight
+template <int R>
+__device__ __forceinline__ void strip_step(CallStrip<R> &cur, const BwdCall<R> &cb, const BwdCall<R> &nb,
+                                           bool valid, float *row, const PairGeom &g) {
+    constexpr int NJ = 2 * R + 2;
+    f32x2 w[NJ];
+    const bool fast = valid && cur.live && cur.fast;
+    if (fast) {
+        const f32x2 *q = reinterpret_cast<const f32x2 *>(row + 2 * (cur.m - R));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) w[j] = q[j];
+    }
+    CallStrip<R> nxt;
+    strip_compute<R>(nxt, nb, g);
+    if (fast) strip_apply_fast<R>(cur, w, row, g);
+    if (valid && cur.live && !cur.fast) strip_apply_slow<R>(cur, cb, row, g);
+    cur = nxt;
+}
+
 // NL = 2 (one level pair) or 4 (two); blockDim = pix * NL / 2.
-template <int R, int NL>
+template <int R, int NL, bool PIPE = true>
 __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArgs a) {
     constexpr int NP = NL / 2, T = 2 * R + 1;
     float *lds = bwd_calls_lds;
@@ -187,6 +315,20 @@ __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArg
         bwd_call_load<R>(b1, a, min(1, last), bimg, rem, go_off);
         bwd_call_load<R>(b2, a, min(2, last), bimg, rem, go_off);
         bwd_call_load<R>(b3, a, min(3, last), bimg, rem, go_off);
+        if constexpr (PIPE) {
+            CallStrip<R> cur;
+            strip_compute<R>(cur, b0, g);
+            for (int c = 0; c < a.ncalls; c += 4) {
+                strip_step<R>(cur, b0, b1, true, row, g);                 // call c
+                bwd_call_load<R>(b0, a, min(c + 4, last), bimg, rem, go_off);
+                strip_step<R>(cur, b1, b2, c + 1 < a.ncalls, row, g);
+                bwd_call_load<R>(b1, a, min(c + 5, last), bimg, rem, go_off);
+                strip_step<R>(cur, b2, b3, c + 2 < a.ncalls, row, g);
+                bwd_call_load<R>(b2, a, min(c + 6, last), bimg, rem, go_off);
+                strip_step<R>(cur, b3, b0, c + 3 < a.ncalls, row, g);     // b0 holds call c + 4
+                bwd_call_load<R>(b3, a, min(c + 7, last), bimg, rem, go_off);
+            }
+        } else
         for (int c = 0; c < a.ncalls; c += 4) {
             bwd_call_add<R>(b0, row, g);
             bwd_call_load<R>(b0, a, min(c + 4, last), bimg, rem, go_off);
@@ -249,6 +391,15 @@ hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int
     const unsigned nblk = (unsigned)((a.P + pix - 1) / pix);
     const size_t lds = (size_t)a.lds_floats * 4;
     const dim3 blk(pix * np);
+#ifdef RAFTCORR_DEV
+    // dev A/B: RAFTCORR_BWDC_VARIANT=1 runs the unpipelined form (two
+    // read-modify-writes per call, no overlap)
+    if (rc::dev_knob("RAFTCORR_BWDC_VARIANT") == 1 && radius == 4) {
+        if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<4, 4, false>), dim3(nblk), blk, lds, s, a);
+        else hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<4, 2, false>), dim3(nblk), blk, lds, s, a);
+        return hipGetLastError();
+    }
+#endif
 #define RC_LBWDC(RR)                                                                                      \
     if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<RR, 4>), dim3(nblk), blk, lds, s, a); \
     else hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<RR, 2>), dim3(nblk), blk, lds, s, a);
