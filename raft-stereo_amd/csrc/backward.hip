@@ -732,18 +732,15 @@ void volume_bwd_kernel(BuildBwdArgs a, int nwg_total) {
 // supplies k = 4g..4g+3 and 16+4g..16+4g+3 of its row to the MFMA's 8-k
 // slot g (the sum over k is order-free; both operands use the same
 // permutation), i.e. two conflict-free ds_read_b128 at row*40 + 4g and +16.
-template <bool VEC, int NLEV>
-__global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a, int nwg_total) {
-    static_assert(NLEV >= kPairFold, "level count");
+template <bool VEC, int NLEV, bool KM, bool K2>
+__device__ __forceinline__ void volume_bwd_split_tile(const BuildBwdArgs &a, float (*smem)[2][BwdTile<32>::IMG],
+                                                      int row, int tile, int T1) {
+    constexpr bool kind2 = K2;                  // false: a dF1 tile, true: a dF2 tile
     typedef BwdTile<32> TL;
     constexpr int kBwdK = 32, kBwdRow = TL::ROW, QPT = TL::QPT;
-    __shared__ __attribute__((aligned(16))) float smem[2][2][TL::IMG];   // [buf][X | Y]
+    constexpr int kYP = 132;                    // KM: pitch of the k-major G image (32 x 132 <= 128 x 40)
+    static_assert(32 * kYP <= TL::IMG, "k-major image fits the operand slot");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wgid = xcd_remap(blockIdx.x, nwg_total);   // one (b,h) row's tiles on one XCD
-    const int T1 = a.tm * a.tn1, T = T1 + a.tm * a.tn2;
-    const int row = wgid / T;
-    int tile = wgid - row * T;
-    const bool kind2 = tile >= T1;              // false: a dF1 tile, true: a dF2 tile
     if (kind2) tile -= T1;
     const int tn = kind2 ? a.tn2 : a.tn1;
     const int tmi = tile / tn, tni = tile - tmi * tn;
@@ -770,6 +767,9 @@ __global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a
             if (!kind2) {
                 const int w1 = n0 + r;
                 fold_load<NLEV>(a, prow0 + w1, kb + kq, w1 < W1, ry[u]);
+            } else if constexpr (KM) {                // G rows, coalesced along w2
+                const int w1 = kb + (c >> 5);
+                fold_load<NLEV>(a, prow0 + w1, n0 + 4 * (c & 31), w1 < W1, ry[u]);
             } else {
                 const int w1 = kb + (c % kBwdK);
                 fold_load<NLEV>(a, prow0 + w1, n0 + 4 * (c / kBwdK), w1 < W1, ry[u]);
@@ -785,6 +785,9 @@ __global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a
             *reinterpret_cast<f32x4 *>(sx + r * kBwdRow + kq) = rx[u];
             if (!kind2) {
                 *reinterpret_cast<f32x4 *>(sy + r * kBwdRow + kq) = fold_math<NLEV>(a, kb + kq, ry[u]);
+            } else if constexpr (KM) {                // k-major image [32 w1][kYP]
+                *reinterpret_cast<f32x4 *>(sy + (c >> 5) * kYP + 4 * (c & 31)) =
+                    fold_math<NLEV>(a, n0 + 4 * (c & 31), ry[u]);
             } else {
                 const int k = c % kBwdK, nq = 4 * (c / kBwdK);
                 const f32x4 gq = fold_math<NLEV>(a, n0 + nq, ry[u]);
@@ -792,6 +795,17 @@ __global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a
                 for (int e = 0; e < 4; ++e) sy[(nq + e) * kBwdRow + k] = gq[e];
             }
         }
+    };
+    // the k-major image's fragment: column n, rows k of slot g (8 dwords;
+    // pitch 132 puts the g and g+1 halves of a 32-lane group 16 banks apart)
+    auto frag_km = [&](const float *img, int n, int g) {
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            x[j] = img[(4 * g + j) * kYP + n];
+            x[4 + j] = img[(16 + 4 * g + j) * kYP + n];
+        }
+        return sp_split(x);
     };
     // a lane's fragment of image row `rr`: k = 4g..4g+3 and 16+4g..16+4g+3
     auto frag = [&](const float *img, int rr, int g) {
@@ -823,7 +837,7 @@ __global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a
         for (int ma = 0; ma < 4; ++ma) bx[ma] = frag(sx, wm + 16 * ma + i16, g);
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) {
-            const SplitFrag ay = frag(sy, wn + 16 * nb + i16, g);
+            const SplitFrag ay = (KM && kind2) ? frag_km(sy, wn + 16 * nb + i16, g) : frag(sy, wn + 16 * nb + i16, g);
 #pragma unroll
             for (int ma = 0; ma < 4; ++ma) sp_mma6(acc[nb][ma], ay, bx[ma]);
         }
@@ -849,6 +863,24 @@ __global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a
             }
         }
     }
+}
+
+
+template <bool VEC, int NLEV, bool KM = true>
+__global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a, int nwg_total) {
+    static_assert(NLEV >= kPairFold, "level count");
+    __shared__ __attribute__((aligned(16))) float smem[2][2][BwdTile<32>::IMG];   // [buf][X | Y]
+    const int wgid = xcd_remap(blockIdx.x, nwg_total);   // one (b,h) row's tiles on one XCD
+    const int T1 = a.tm * a.tn1, T = T1 + a.tm * a.tn2;
+    const int row = wgid / T;
+    const int tile = wgid - row * T;
+    const bool kind2 = tile >= T1;              // false: a dF1 tile, true: a dF2 tile
+#ifdef RAFTCORR_DEV
+    if ((a.dev_only == 1 && kind2) || (a.dev_only == 2 && !kind2)) return;   // timing probe
+#endif
+    // one instantiation per GEMM, so each is register-allocated on its own
+    if (kind2) volume_bwd_split_tile<VEC, NLEV, KM, true>(a, smem, row, tile, T1);
+    else volume_bwd_split_tile<VEC, NLEV, KM, false>(a, smem, row, tile, T1);
 }
 
 }  // namespace rc
@@ -930,7 +962,11 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
     return hipGetLastError();
 }
 
-hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s) {
+hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a_in, hipStream_t s) {
+    rc::BuildBwdArgs a = a_in;
+#ifdef RAFTCORR_DEV
+    a.dev_only = rc::dev_knob("RAFTCORR_VBWD_ONLY");
+#endif
     const long long nwg = (long long)a.B * a.H * a.tm * (a.tn1 + a.tn2);
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
@@ -944,6 +980,12 @@ hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s) {
     // kernel)
     const bool pairfold = a.nlev == 3 && a.g[1] == nullptr;
     if (!a.exact && vec && (pairfold || a.nlev == 1 || a.nlev == 2)) {
+#ifdef RAFTCORR_DEV
+        if (pairfold && rc::dev_knob("RAFTCORR_VBWD_VARIANT") == 2) {   // dev A/B: G^T staged by scattered loads
+            hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, rc::kPairFold, false>), grid, blk, 0, s, a, (int)nwg);
+            return hipGetLastError();
+        }
+#endif
         if (pairfold) hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, rc::kPairFold>), grid, blk, 0, s, a, (int)nwg);
         else if (a.nlev == 1) hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, 1>), grid, blk, 0, s, a, (int)nwg);
         else hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, 2>), grid, blk, 0, s, a, (int)nwg);

@@ -179,6 +179,7 @@ struct BuildBwdArgs {
     int pow2;
     long long shadow[kMaxLevels];   // floats from g[l] to its RC_SHADOW copy (kPairFold), 0 = none
     int exact;                      // 1: exact fp32 MFMA kernel (RC_BUILD_EXACT_F32); 0: split-bf16
+    int dev_only;                   // dev library timing probe: 1 = dF1 tiles only, 2 = dF2 only
 };
 
 }  // namespace rc

@@ -176,3 +176,20 @@ def test_pyr_dtype_flag_bits_validated():
                               None) == _lib.RC_EINVAL
     assert L.rc_corr_lookup_step(two, w2, None, junk, 2, 4, 1, f(0x2000), None, f(0x3000), f(0x5000),
                                  1, 1, 64, f(0x4000), None) == _lib.RC_EINVAL
+
+
+def test_build_backward_exact_flag():
+    """ABI v8: rc_corr_build_backward takes RC_BUILD_EXACT_F32 in fmap_dtype
+    (the exact fp32 MFMA kernel instead of the split-bf16 one); any other
+    dtype or flag bit is refused before a launch.  B = 0 returns after the
+    dtype check without touching memory."""
+    L = _lib.lib()
+    f = lambda a: ctypes.c_void_p(a)  # noqa: E731
+    g = _lib.ptr_array([f(0x1000)])
+    bb = lambda dt, B: L.rc_corr_build_backward(  # noqa: E731
+        f(0x1000), f(0x2000), dt, B, 32, 2, 64, 64, g, None, 1, f(0x3000), f(0x4000), None)
+    assert bb(_lib.RC_F32 | _lib.RC_BUILD_EXACT_F32, 0) == _lib.RC_OK
+    assert bb(_lib.RC_F32, 0) == _lib.RC_OK
+    assert bb(_lib.RC_BF16, 0) == _lib.RC_EUNSUPPORTED
+    assert bb(_lib.RC_F32 | 0x400000, 0) == _lib.RC_EUNSUPPORTED
+    assert L.rc_last_error()
