@@ -40,6 +40,8 @@
 // Measured and not kept: the row updates as LDS-side adds (ds_add_f32, no
 // read on the lane's chain; same order): 2499 vs 669 us per 32-call launch
 // at config 2 (r03m).
+#include <algorithm>
+
 #include "common.h"
 
 namespace rc {
@@ -361,6 +363,130 @@ __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArg
     }
 }
 
+// ---- compact rows (wide rows, r03t) -------------------------------------------
+// The kernel above gives every (pixel, level pair) lane its whole gradient
+// row in LDS (1.36 KB per pixel at W2 = 240), so a CU holds 3 waves and the
+// lanes' serial call chains are not hidden.  A call only touches the window
+// [2(m-R), 2(m+R+2)) of its lane's row (plus, on the rare tap-by-tap path,
+// in-row elements near it), so each lane first reads its calls' x and keeps
+// only the union of its windows, [lo, hi), in LDS: ~70 floats per lane at
+// the bench coordinates instead of 170.  A block is ONE wave (64 lanes); the
+// lanes' ranges are packed in lane order into `budget` floats, in as many
+// passes as they need (one at the bench coordinates; a pass runs its lanes'
+// calls and writes their rows while the other lanes wait), so any
+// coordinates stay correct.  Rows are written whole (zeros outside [lo, hi)
+// in overwrite mode).  The per-call updates are strip_step's in the same
+// order: bit-identical to the whole-row kernel.  At W2 = 240 it measured
+// slower than the whole-row kernel (692-815 vs 633-760 us: 8 waves per CU
+// instead of 3 did not help -- the lanes' VALU work and LDS bank conflicts,
+// not their latency, set the pace), so the launcher takes it only for rows
+// too wide for whole-row blocks of a full wave.
+template <int R, int NL>
+__global__ __launch_bounds__(64) void lookup_bwd_calls_compact_kernel(LookupBwdCallsArgs a) {
+    constexpr int NP = NL / 2, T = 2 * R + 1;
+    float *lds = bwd_calls_lds;
+    const int lane = threadIdx.x;
+    const int pix = 64 / NP;
+    const long long pblk = (long long)blockIdx.x * pix;
+    const int npix = (int)min((long long)pix, a.P - pblk);
+    const int k = lane / pix, i = lane - k * pix;
+    const bool active = k < NP && i < npix;
+    const int lo = 2 * k;
+    PairGeom g;
+    g.Wlo = a.W[lo];
+    g.Whi = a.W[lo + 1];
+    g.slo = 1.0f / (float)(1 << lo);
+    g.shi = 0.5f * g.slo;
+    g.halflo = (float)(g.Wlo - 1) / 2.0f;
+    g.halfhi = (float)(g.Whi - 1) / 2.0f;
+    g.dvlo = div_prep((float)(g.Wlo - 1));
+    g.dvhi = div_prep((float)(g.Whi - 1));
+    const long long p = pblk + (active ? i : 0), bimg = p / a.HW, rem = p - bimg * a.HW;
+
+    // 1. the lane's element range: the union over its live calls of
+    //    [2m - 2R - 4, 2m + 2R + 8) (the window and the tap-by-tap path's
+    //    elements, |n - 2m| <= 2), 16-B aligned
+    int rlo = 0x3FFFFFFF, rhi = -0x3FFFFFFF;
+    if (active) {
+        for (int c = 0; c < a.ncalls; ++c) {
+            const float xhi = a.coords[c][bimg * a.cbs[c] + rem] * g.shi;
+            if (xhi > -(float)(R + 4) && xhi < (float)(g.Whi + R + 4)) {   // false for NaN
+                const int m = (int)floorf(xhi);
+                if (m >= -R - 2 && m <= g.Whi + R) {
+                    rlo = min(rlo, 2 * m - 2 * R - 4);
+                    rhi = max(rhi, 2 * m + 2 * R + 8);
+                }
+            }
+        }
+    }
+    int S = 0;
+    if (rlo <= rhi) {
+        rlo = rlo & ~3;                            // floor to a multiple of 4 (two's complement)
+        S = (rhi - rlo + 3) & ~3;
+    } else {
+        rlo = 0;
+    }
+    // 2. pack the lanes' ranges into passes of `budget` floats, in lane order
+    int my_off = 0, my_pass = 0, npass = 1;
+    {
+        int cur = 0, pass = 0;
+        for (int l = 0; l < 64; ++l) {
+            const int sl = __shfl(S, l, 64);
+            if (cur + sl > a.budget) { ++pass; cur = 0; }
+            if (lane == l) { my_off = cur; my_pass = pass; }
+            cur += sl;
+        }
+        npass = pass + 1;
+    }
+    const long long go_off = (bimg * (NL * T) + lo * T) * (long long)a.HW + rem;
+    const int last = a.ncalls - 1;
+    for (int ps = 0; ps < npass; ++ps) {
+        // zero the budget (one wave: LDS runs its operations in order)
+        for (int f = 4 * lane; f < a.budget; f += 256)
+            *reinterpret_cast<f32x4 *>(lds + f) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (active && my_pass == ps && S > 0) {
+            float *row = lds + my_off - rlo;           // row[e] = element e of the lane's row
+            BwdCall<R> b0, b1, b2, b3;
+            bwd_call_load<R>(b0, a, 0, bimg, rem, go_off);
+            bwd_call_load<R>(b1, a, min(1, last), bimg, rem, go_off);
+            bwd_call_load<R>(b2, a, min(2, last), bimg, rem, go_off);
+            bwd_call_load<R>(b3, a, min(3, last), bimg, rem, go_off);
+            CallStrip<R> cur;
+            strip_compute<R>(cur, b0, g);
+            for (int c = 0; c < a.ncalls; c += 4) {
+                strip_step<R>(cur, b0, b1, true, row, g);
+                bwd_call_load<R>(b0, a, min(c + 4, last), bimg, rem, go_off);
+                strip_step<R>(cur, b1, b2, c + 1 < a.ncalls, row, g);
+                bwd_call_load<R>(b1, a, min(c + 5, last), bimg, rem, go_off);
+                strip_step<R>(cur, b2, b3, c + 2 < a.ncalls, row, g);
+                bwd_call_load<R>(b2, a, min(c + 6, last), bimg, rem, go_off);
+                strip_step<R>(cur, b3, b0, c + 3 < a.ncalls, row, g);
+                bwd_call_load<R>(b3, a, min(c + 7, last), bimg, rem, go_off);
+            }
+        }
+        // 3. write back this pass's rows: one row per step, the wave's lanes
+        //    along it in 16-B chunks
+        for (int l = 0; l < 64; ++l) {
+            const int lp = __shfl(my_pass, l, 64), la = __shfl(active ? 1 : 0, l, 64);
+            if (!la || lp != ps) continue;             // wave-uniform
+            const int kk = l / pix, ii = l - kk * pix;
+            const int llo = __shfl(rlo, l, 64), lS = __shfl(S, l, 64), loff = __shfl(my_off, l, 64);
+            const int n4 = a.wout[kk] >> 2;
+            f32x4 *dst = reinterpret_cast<f32x4 *>(a.g[kk] + (pblk + ii) * a.ld[kk]);
+            for (int c4 = lane; c4 < n4; c4 += 64) {
+                const int e = 4 * c4 - llo;            // element offset inside the range
+                const bool in = e >= 0 && e < lS;
+                const f32x4 v = in ? *reinterpret_cast<const f32x4 *>(lds + loff + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+                if (a.accumulate) {
+                    if (in) dst[c4] = dst[c4] + v;
+                } else {
+                    dst[c4] = v;
+                }
+            }
+        }
+    }
+}
+
 }  // namespace rc
 
 // LDS per workgroup: pair k holds pix rows of S_k = round4(W_2k) + M floats
@@ -370,6 +496,47 @@ hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int
     if (a.P <= 0 || a.ncalls <= 0) return hipSuccess;
     if (a.ncalls > rc::kMaxBwdCalls || (levels != 2 && levels != 4) || radius < 1 || radius > 4)
         return hipErrorInvalidValue;
+    {
+        // compact rows: one wave per block, `budget` floats of LDS: at least
+        // twice the widest possible lane range (W + 8R + 24) and 20 KB
+        // (8 blocks per CU)
+        const int np = levels / 2;
+        int maxS = 0;
+        for (int k = 0; k < np; ++k) {
+            maxS = std::max(maxS, ((a.W[2 * k] + 8 * radius + 24) + 3) & ~3);
+            a.wout[k] = (a.W[2 * k] + 3) & ~3;     // columns written per row (padding as zeros)
+        }
+        a.budget = std::max(5120, 2 * maxS);
+        a.pix = 64 / np;
+        // the whole-row kernel while a block of its 64 lanes holds whole rows
+        // in 64 KB (W2 = 240: 43.5 KB; measured faster there, 633-760 vs
+        // 692-815 us, r03u/r03v); compact rows for wider rows, where whole
+        // rows would leave blocks of 8-16 pixels
+        int per_pix_whole = 0;
+        for (int k = 0; k < np; ++k) per_pix_whole += ((a.W[2 * k] + 3) & ~3) + 4 * radius + 4;
+        bool use_compact = (long long)(per_pix_whole * (64 / np) + np * (4 * radius + 4)) * 4 > 65536;
+#ifdef RAFTCORR_DEV
+        const int dv = rc::dev_knob("RAFTCORR_BWDC_VARIANT");   // dev A/B: 0 = the launcher's choice,
+        if (dv == 3) use_compact = true;                         // 3 = compact, 1 / 2 = whole rows
+        if (dv == 1 || dv == 2) use_compact = false;
+#endif
+        if (use_compact && (long long)a.budget * 4 <= 65536) {
+            const unsigned nblk = (unsigned)((a.P + a.pix - 1) / a.pix);
+            const size_t lds = (size_t)a.budget * 4;
+#define RC_LBWDCC(RR)                                                                                                 \
+    if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_compact_kernel<RR, 4>), dim3(nblk), dim3(64), lds, s, a); \
+    else hipLaunchKernelGGL((rc::lookup_bwd_calls_compact_kernel<RR, 2>), dim3(nblk), dim3(64), lds, s, a);
+            switch (radius) {
+                case 1: RC_LBWDCC(1) break;
+                case 2: RC_LBWDCC(2) break;
+                case 3: RC_LBWDCC(3) break;
+                case 4: RC_LBWDCC(4) break;
+            }
+#undef RC_LBWDCC
+            return hipGetLastError();
+        }
+    }
+
     const int np = levels / 2, M = 4 * radius + 4;
     int per_pix = 0;
     for (int k = 0; k < np; ++k) {
@@ -392,9 +559,9 @@ hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int
     const size_t lds = (size_t)a.lds_floats * 4;
     const dim3 blk(pix * np);
 #ifdef RAFTCORR_DEV
-    // dev A/B: RAFTCORR_BWDC_VARIANT=1 runs the unpipelined form (two
-    // read-modify-writes per call, no overlap)
-    if (rc::dev_knob("RAFTCORR_BWDC_VARIANT") == 1 && radius == 4) {
+    // dev A/B: RAFTCORR_BWDC_VARIANT=1 runs the whole-row pipelined kernel,
+    // 2 the whole-row unpipelined form (two read-modify-writes per call)
+    if (rc::dev_knob("RAFTCORR_BWDC_VARIANT") == 2 && radius == 4) {
         if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<4, 4, false>), dim3(nblk), blk, lds, s, a);
         else hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<4, 2, false>), dim3(nblk), blk, lds, s, a);
         return hipGetLastError();

@@ -158,6 +158,7 @@ struct LookupBwdCallsArgs {
     int pix;                  // pixels per workgroup
     int ncalls;               // 1..kMaxBwdCalls
     int accumulate;           // 0: overwrite the rows; 1: add to them
+    int budget;               // compact kernel: LDS floats per block (one wave)
     long long P;
     int HW;
     const float *coords[kMaxBwdCalls];

@@ -118,9 +118,10 @@ def test_calls_accumulate_adds_to_buffers():
 
 @pytest.mark.parametrize("case", ["wide", "per_level"])
 def test_calls_fallbacks_match_per_call(case):
-    """Rows too wide for 64 KB of LDS at 8 pixels (W2 = 2600), and the per-level
-    layout (3 levels), go through per-call launches (zeroed first in overwrite
-    mode): the same sums as the per-call entry point, bit for bit."""
+    """Rows too wide for the whole-row kernel (W2 = 2600: the compact kernel
+    keeps only each lane's touched range, so it serves them; same sums up to
+    association), and the per-level layout (3 levels: per-call launches,
+    zeroed first in overwrite mode -- the per-call sums bit for bit)."""
     if case == "wide":
         B, H, W1, W2, L, r, calls, pair = 1, 2, 16, 2600, 4, 4, 3, True
     else:
@@ -141,7 +142,10 @@ def test_calls_fallbacks_match_per_call(case):
         rcorr.lookup_backward(b, c, go, L, r)
     for ta, tb in zip(a, b):
         if ta is not None:
-            assert torch.equal(ta, tb)
+            if case == "per_level":
+                assert torch.equal(ta, tb)
+            else:
+                assert norm_err(ta.cpu().numpy(), tb.cpu().numpy()) <= 1e-6
 
 
 @pytest.mark.parametrize("L", [2, 4])
@@ -164,3 +168,37 @@ def test_autograd_deferred_equals_per_call(L):
         grads[deferred] = (a.grad.cpu().numpy(), b.grad.cpu().numpy())
     for x, y in zip(grads[True], grads[False]):
         assert norm_err(x, y) <= 1e-5 and rel_l2(x, y) <= 1e-6
+
+
+@pytest.mark.parametrize("spread", ["bench", "whole_row"])
+def test_compact_equals_whole_row_kernel(spread):
+    """The compact-row kernel (RAFTCORR_BWDC_VARIANT=3; the launcher's choice
+    for wide rows) against the whole-row kernel (=1), bit for bit: at the bench's
+    coordinates (one pass) and with x spread over the whole row (every lane
+    needs its full row: several passes per block)."""
+    import os
+    from raft_stereo_amd import _lib
+    B, H, W1, W2, L, r, calls = 2, 3, 60, 240, 4, 4, 12
+    g = torch.Generator().manual_seed(11 if spread == "bench" else 12)
+    cs, gs = make_calls(B, H, W1, W2, L, r, calls, seed=21 if spread == "bench" else 22)
+    if spread == "whole_row":
+        for c in cs:
+            c[:, 0] = torch.rand(B, H, W1, generator=g) * (W2 + 20) - 10
+    cd = [c.to(DEV) for c in cs]
+    gd = [x.to(DEV) for x in gs]
+    P = B * H * W1
+    widths = [W2 >> i for i in range(L)]
+    out = {}
+    with _lib.dev_library():
+        for v in ("3", "1"):
+            os.environ["RAFTCORR_BWDC_VARIANT"] = v
+            buf = rcorr.grad_buffers(P, widths, torch.device(DEV), pair=True, zero=False)
+            for t in buf:
+                if t is not None:
+                    (t._base if t._base is not None else t).fill_(float("nan"))
+            rcorr.lookup_backward_calls(buf, cd, gd, L, r, overwrite=True)
+            out[v] = buf
+        os.environ["RAFTCORR_BWDC_VARIANT"] = "0"
+    for ta, tb in zip(out["3"], out["1"]):
+        if ta is not None:
+            assert torch.equal(ta, tb)

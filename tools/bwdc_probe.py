@@ -2,9 +2,10 @@
 
     python tools/bwdc_probe.py [--config sceneflow] [--rounds 7]
 
-Variant 0 = the product (software-pipelined, one window read-modify-write
-per call), 1 = the round-3 first version (RAFTCORR_BWDC_VARIANT=1: two
-read-modify-writes per call, no overlap), through libraftcorr_dev.so,
+Variant 3 = compact rows (each lane keeps only the range its calls touch;
+the launcher's choice for wide rows), 1 = whole rows, software-pipelined
+(the launcher's choice at W2 = 240), 2 = whole rows, two read-modify-writes
+per call, no overlap (RAFTCORR_BWDC_VARIANT), through libraftcorr_dev.so,
 interleaved in one process on the bench workload (32 calls, one output
 gradient per call).  Prints median microseconds per launch and whether the
 two write the same gradient rows bit for bit.
@@ -37,11 +38,11 @@ def main():
     gl = [torch.randn(B, L * (2 * r + 1), H, W1, generator=g).to(dev) for _ in range(iters)]
     P = B * H * W1
     widths = [W2 >> i for i in range(L)]
-    bufs = {v: rcorr.grad_buffers(P, widths, dev, pair=True, zero=False) for v in (0, 1)}
-    times = {0: [], 1: []}
+    bufs = {v: rcorr.grad_buffers(P, widths, dev, pair=True, zero=False) for v in (3, 1, 2)}
+    times = {3: [], 1: [], 2: []}
     with _lib.dev_library():
         for rd in range(a.rounds + 1):
-            for v in (0, 1):
+            for v in (3, 1, 2):
                 os.environ["RAFTCORR_BWDC_VARIANT"] = str(v)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
@@ -52,10 +53,12 @@ def main():
                 if rd:
                     times[v].append(e0.elapsed_time(e1) * 1e3)
         os.environ["RAFTCORR_BWDC_VARIANT"] = "0"
-    same = all(torch.equal(x, y) for x, y in zip(bufs[0], bufs[1]) if x is not None)
+    same = all(torch.equal(x, y) and torch.equal(x, z)
+               for x, y, z in zip(bufs[3], bufs[1], bufs[2]) if x is not None)
     print(json.dumps({"config": a.config, "calls": iters,
-                      "pipelined_us": statistics.median(times[0]),
-                      "unpipelined_us": statistics.median(times[1]), "bit_identical": same}))
+                      "compact_us": statistics.median(times[3]),
+                      "whole_row_pipelined_us": statistics.median(times[1]),
+                      "whole_row_unpipelined_us": statistics.median(times[2]), "bit_identical": same}))
 
 
 if __name__ == "__main__":
