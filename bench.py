@@ -359,7 +359,7 @@ def backward_timing(cfg, f1, f2, coords, reps=3):
             "bound": "hbm", "achieved": cbytes / (lc_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": cbytes / (lc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "algorithmic_bytes": cbytes, "calls_per_launch": iters,
-            "kernel": f"rc::lookup_bwd_calls_kernel<{r},{L},true>"}
+            "kernel": f"rc::lookup_bwd_calls_compact_kernel<{r},{L}>"}
     return out
 
 

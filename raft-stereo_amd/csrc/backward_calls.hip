@@ -54,16 +54,26 @@ struct BwdCall {
     float gv[2][2 * R + 1];   // output gradients of levels 2k and 2k+1
 };
 
-template <int R>
+// One call's x and output gradients for this lane's (pixel, level pair):
+// buffer loads through a per-call resource (wave-uniform base), the lane's
+// offset in a VGPR and each channel's plane offset in an SGPR -- no 64-bit
+// address arithmetic per load.
+template <int R, int NL>
 __device__ __forceinline__ void bwd_call_load(BwdCall<R> &c, const LookupBwdCallsArgs &a, int call,
                                               long long bimg, long long rem, long long go_off) {
     constexpr int T = 2 * R + 1;
-    c.x = a.coords[call][bimg * a.cbs[call] + rem];
-    const float *go = a.grad_out[call] + go_off;
+    const long long nb = a.P / a.HW;
+    const auto rx = make_rsrc(a.coords[call], clamp_bytes(((nb - 1) * a.cbs[call] + a.HW) * 4));
+    c.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                        rx, (int)(uint32_t)((bimg * a.cbs[call] + rem) * 4), 0, 0));
+    const auto rg = make_rsrc(a.grad_out[call], clamp_bytes(a.P * (NL * T) * 4));
+    const uint32_t vo = (uint32_t)(go_off * 4);
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
-        for (int t = 0; t < T; ++t) c.gv[e][t] = go[(long long)(e * T + t) * a.HW];
+        for (int t = 0; t < T; ++t)
+            c.gv[e][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      rg, (int)vo, (e * T + t) * a.HW * 4, 0));
 }
 
 struct PairGeom {
@@ -215,17 +225,21 @@ __device__ __forceinline__ void strip_apply_fast(const CallStrip<R> &s, f32x2 (&
                                                  const PairGeom &g) {
     constexpr int NJ = 2 * R + 2;
     const int jb = s.m - R, ib = 2 * s.m + s.dd - R;
+    // in-row masks as one unsigned range test per element: j in [-jb, Whi - jb)
+    const unsigned uwhi = (unsigned)g.Whi, uwlo = (unsigned)g.Wlo;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {                  // level 2k+1: c/2 to both children
-        const float v = (jb + j >= 0 && jb + j < g.Whi) ? s.s1[j] : 0.0f;
+        const float v = (unsigned)(jb + j) < uwhi ? s.s1[j] : 0.0f;
         w[j][0] += v;
         w[j][1] += v;
     }
+    float s0m[NJ];                                  // level-2k strip, zero outside the row
 #pragma unroll
-    for (int k = 0; k < 2 * NJ; ++k) {              // level 2k: window element k = dd + R + j
-        const int j0 = k - R, j1 = k - R - 1;
-        const float v0 = (j0 >= 0 && j0 < NJ && ib + j0 >= 0 && ib + j0 < g.Wlo) ? s.s0[j0 < 0 ? 0 : (j0 >= NJ ? NJ - 1 : j0)] : 0.0f;
-        const float v1 = (j1 >= 0 && j1 < NJ && ib + j1 >= 0 && ib + j1 < g.Wlo) ? s.s0[j1 < 0 ? 0 : (j1 >= NJ ? NJ - 1 : j1)] : 0.0f;
+    for (int j = 0; j < NJ; ++j) s0m[j] = (unsigned)(ib + j) < uwlo ? s.s0[j] : 0.0f;
+#pragma unroll
+    for (int k = R; k <= R + NJ; ++k) {             // level 2k: window element k = dd + R + j
+        const float v0 = k - R < NJ ? s0m[k - R < NJ ? k - R : 0] : 0.0f;
+        const float v1 = k - R - 1 >= 0 ? s0m[k - R - 1 >= 0 ? k - R - 1 : 0] : 0.0f;
         w[k >> 1][k & 1] += s.dd ? v1 : v0;
     }
     f32x2 *q = reinterpret_cast<f32x2 *>(row + 2 * (s.m - R));
@@ -313,33 +327,33 @@ __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArg
         const long long go_off = (bimg * (NL * T) + lo * T) * (long long)a.HW + rem;
         const int last = a.ncalls - 1;
         BwdCall<R> b0, b1, b2, b3;
-        bwd_call_load<R>(b0, a, 0, bimg, rem, go_off);
-        bwd_call_load<R>(b1, a, min(1, last), bimg, rem, go_off);
-        bwd_call_load<R>(b2, a, min(2, last), bimg, rem, go_off);
-        bwd_call_load<R>(b3, a, min(3, last), bimg, rem, go_off);
+        bwd_call_load<R, NL>(b0, a, 0, bimg, rem, go_off);
+        bwd_call_load<R, NL>(b1, a, min(1, last), bimg, rem, go_off);
+        bwd_call_load<R, NL>(b2, a, min(2, last), bimg, rem, go_off);
+        bwd_call_load<R, NL>(b3, a, min(3, last), bimg, rem, go_off);
         if constexpr (PIPE) {
             CallStrip<R> cur;
             strip_compute<R>(cur, b0, g);
             for (int c = 0; c < a.ncalls; c += 4) {
                 strip_step<R>(cur, b0, b1, true, row, g);                 // call c
-                bwd_call_load<R>(b0, a, min(c + 4, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b0, a, min(c + 4, last), bimg, rem, go_off);
                 strip_step<R>(cur, b1, b2, c + 1 < a.ncalls, row, g);
-                bwd_call_load<R>(b1, a, min(c + 5, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b1, a, min(c + 5, last), bimg, rem, go_off);
                 strip_step<R>(cur, b2, b3, c + 2 < a.ncalls, row, g);
-                bwd_call_load<R>(b2, a, min(c + 6, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b2, a, min(c + 6, last), bimg, rem, go_off);
                 strip_step<R>(cur, b3, b0, c + 3 < a.ncalls, row, g);     // b0 holds call c + 4
-                bwd_call_load<R>(b3, a, min(c + 7, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b3, a, min(c + 7, last), bimg, rem, go_off);
             }
         } else
         for (int c = 0; c < a.ncalls; c += 4) {
             bwd_call_add<R>(b0, row, g);
-            bwd_call_load<R>(b0, a, min(c + 4, last), bimg, rem, go_off);
+            bwd_call_load<R, NL>(b0, a, min(c + 4, last), bimg, rem, go_off);
             if (c + 1 < a.ncalls) bwd_call_add<R>(b1, row, g);
-            bwd_call_load<R>(b1, a, min(c + 5, last), bimg, rem, go_off);
+            bwd_call_load<R, NL>(b1, a, min(c + 5, last), bimg, rem, go_off);
             if (c + 2 < a.ncalls) bwd_call_add<R>(b2, row, g);
-            bwd_call_load<R>(b2, a, min(c + 6, last), bimg, rem, go_off);
+            bwd_call_load<R, NL>(b2, a, min(c + 6, last), bimg, rem, go_off);
             if (c + 3 < a.ncalls) bwd_call_add<R>(b3, row, g);
-            bwd_call_load<R>(b3, a, min(c + 7, last), bimg, rem, go_off);
+            bwd_call_load<R, NL>(b3, a, min(c + 7, last), bimg, rem, go_off);
         }
     }
     __syncthreads();
@@ -363,7 +377,7 @@ __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArg
     }
 }
 
-// ---- compact rows (wide rows, r03t) -------------------------------------------
+// ---- compact rows (the product since r03y) ----------------------------------
 // The kernel above gives every (pixel, level pair) lane its whole gradient
 // row in LDS (1.36 KB per pixel at W2 = 240), so a CU holds 3 waves and the
 // lanes' serial call chains are not hidden.  A call only touches the window
@@ -376,11 +390,10 @@ __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArg
 // calls and writes their rows while the other lanes wait), so any
 // coordinates stay correct.  Rows are written whole (zeros outside [lo, hi)
 // in overwrite mode).  The per-call updates are strip_step's in the same
-// order: bit-identical to the whole-row kernel.  At W2 = 240 it measured
-// slower than the whole-row kernel (692-815 vs 633-760 us: 8 waves per CU
-// instead of 3 did not help -- the lanes' VALU work and LDS bank conflicts,
-// not their latency, set the pace), so the launcher takes it only for rows
-// too wide for whole-row blocks of a full wave.
+// order: bit-identical to the whole-row kernel.  (With 64-bit address
+// arithmetic per load it measured slower than the whole-row kernel at
+// W2 = 240, 692-815 vs 633-760 us; with per-call buffer resources the 8
+// waves per CU pay: 527 vs 681 us.)
 template <int R, int NL>
 __global__ __launch_bounds__(64) void lookup_bwd_calls_compact_kernel(LookupBwdCallsArgs a) {
     constexpr int NP = NL / 2, T = 2 * R + 1;
@@ -447,21 +460,21 @@ __global__ __launch_bounds__(64) void lookup_bwd_calls_compact_kernel(LookupBwdC
         if (active && my_pass == ps && S > 0) {
             float *row = lds + my_off - rlo;           // row[e] = element e of the lane's row
             BwdCall<R> b0, b1, b2, b3;
-            bwd_call_load<R>(b0, a, 0, bimg, rem, go_off);
-            bwd_call_load<R>(b1, a, min(1, last), bimg, rem, go_off);
-            bwd_call_load<R>(b2, a, min(2, last), bimg, rem, go_off);
-            bwd_call_load<R>(b3, a, min(3, last), bimg, rem, go_off);
+            bwd_call_load<R, NL>(b0, a, 0, bimg, rem, go_off);
+            bwd_call_load<R, NL>(b1, a, min(1, last), bimg, rem, go_off);
+            bwd_call_load<R, NL>(b2, a, min(2, last), bimg, rem, go_off);
+            bwd_call_load<R, NL>(b3, a, min(3, last), bimg, rem, go_off);
             CallStrip<R> cur;
             strip_compute<R>(cur, b0, g);
             for (int c = 0; c < a.ncalls; c += 4) {
                 strip_step<R>(cur, b0, b1, true, row, g);
-                bwd_call_load<R>(b0, a, min(c + 4, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b0, a, min(c + 4, last), bimg, rem, go_off);
                 strip_step<R>(cur, b1, b2, c + 1 < a.ncalls, row, g);
-                bwd_call_load<R>(b1, a, min(c + 5, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b1, a, min(c + 5, last), bimg, rem, go_off);
                 strip_step<R>(cur, b2, b3, c + 2 < a.ncalls, row, g);
-                bwd_call_load<R>(b2, a, min(c + 6, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b2, a, min(c + 6, last), bimg, rem, go_off);
                 strip_step<R>(cur, b3, b0, c + 3 < a.ncalls, row, g);
-                bwd_call_load<R>(b3, a, min(c + 7, last), bimg, rem, go_off);
+                bwd_call_load<R, NL>(b3, a, min(c + 7, last), bimg, rem, go_off);
             }
         }
         // 3. write back this pass's rows: one row per step, the wave's lanes
@@ -496,6 +509,11 @@ hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int
     if (a.P <= 0 || a.ncalls <= 0) return hipSuccess;
     if (a.ncalls > rc::kMaxBwdCalls || (levels != 2 && levels != 4) || radius < 1 || radius > 4)
         return hipErrorInvalidValue;
+    // per-call buffer resources address each output gradient and coords
+    // tensor with 32-bit offsets (larger ones: the caller's per-call path)
+    if (a.P * levels * (2 * radius + 1) * 4 >= 0xFFFFFF00LL) return hipErrorNotSupported;
+    for (int c = 0; c < a.ncalls; ++c)
+        if (((a.P / a.HW - 1) * a.cbs[c] + a.HW) * 4 >= 0xFFFFFF00LL) return hipErrorNotSupported;
     {
         // compact rows: one wave per block, `budget` floats of LDS: at least
         // twice the widest possible lane range (W + 8R + 24) and 20 KB
@@ -508,13 +526,9 @@ hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int
         }
         a.budget = std::max(5120, 2 * maxS);
         a.pix = 64 / np;
-        // the whole-row kernel while a block of its 64 lanes holds whole rows
-        // in 64 KB (W2 = 240: 43.5 KB; measured faster there, 633-760 vs
-        // 692-815 us, r03u/r03v); compact rows for wider rows, where whole
-        // rows would leave blocks of 8-16 pixels
-        int per_pix_whole = 0;
-        for (int k = 0; k < np; ++k) per_pix_whole += ((a.W[2 * k] + 3) & ~3) + 4 * radius + 4;
-        bool use_compact = (long long)(per_pix_whole * (64 / np) + np * (4 * radius + 4)) * 4 > 65536;
+        // compact rows by default (with buffer loads per call: 527 vs 681 us
+        // for whole rows at W2 = 240, 1195 vs 2591 at W2 = 720, r03w/r03y)
+        bool use_compact = true;
 #ifdef RAFTCORR_DEV
         const int dv = rc::dev_knob("RAFTCORR_BWDC_VARIANT");   // dev A/B: 0 = the launcher's choice,
         if (dv == 3) use_compact = true;                         // 3 = compact, 1 / 2 = whole rows

@@ -3,8 +3,7 @@
     python tools/bwdc_probe.py [--config sceneflow] [--rounds 7]
 
 Variant 3 = compact rows (each lane keeps only the range its calls touch;
-the launcher's choice for wide rows), 1 = whole rows, software-pipelined
-(the launcher's choice at W2 = 240), 2 = whole rows, two read-modify-writes
+the product), 1 = whole rows, software-pipelined, 2 = whole rows, two read-modify-writes
 per call, no overlap (RAFTCORR_BWDC_VARIANT), through libraftcorr_dev.so,
 interleaved in one process on the bench workload (32 calls, one output
 gradient per call).  Prints median microseconds per launch and whether the
