@@ -756,12 +756,53 @@ __device__ __forceinline__ void volume_bwd_split_tile(const BuildBwdArgs &a, flo
     constexpr int QR = kBwdK / 4;
     f32x4 rx[QPT];
     FoldRaw<NLEV> ry[QPT];
+    // buffer loads (pair-folded / one-level gradients, the product layouts):
+    // wave-uniform resources over the image's feature map and the gradient
+    // levels, 32-bit offsets, out-of-range offsets read zeros -- no 64-bit
+    // address arithmetic and no branch per load (the launcher keeps every
+    // operand below 4 GiB)
+    constexpr bool BUF = VEC && (NLEV == kPairFold || NLEV == 1);
+    const auto rX = make_rsrc(X + (long long)b * D * H * K, clamp_bytes((long long)D * H * K * 4));
+    const long long Prow = (long long)a.B * a.H * W1;
+    const auto rG0 = make_rsrc(a.g[0], clamp_bytes((Prow * a.ld[0] + a.shadow[0]) * 4));
+    const auto rG2 = make_rsrc(NLEV == kPairFold ? a.g[2] : a.g[0],
+                               clamp_bytes(NLEV == kPairFold ? (Prow * a.ld[2] + a.shadow[2]) * 4 : 0));
+    auto fold_buf = [&](long long prow, int w2, bool ok, FoldRaw<NLEV> &rr) {
+        ok = ok && w2 < a.W2;
+        const uint32_t o0 = ok ? (uint32_t)((prow * a.ld[0] + w2) * 4) : 0xFFFFFF00u;
+        rr.g0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rG0, (int)o0, 0, 0));
+        rr.l1[0] = rr.l1[1] = 0.0f;
+        if (a.shadow[0])         // wave-uniform: RC_SHADOW gradient copies sum
+            rr.g0 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rG0, (int)o0, (int)(a.shadow[0] * 4), 0));
+        if constexpr (NLEV == kPairFold) {
+            const int k2 = w2 >> 2;
+            const uint32_t o2 = ok && k2 < a.Wl[2] ? (uint32_t)((prow * a.ld[2] + k2) * 4) : 0xFFFFFF00u;
+            float v = ld1(rG2, o2);
+            if (a.shadow[2]) v = v + __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                 rG2, (int)o2, (int)(a.shadow[2] * 4), 0));
+            rr.lc[0] = v;
+        }
+    };
     auto load_stage = [&](int kb) {
 #pragma unroll
         for (int u = 0; u < QPT; ++u) {
             const int c = tid + 256 * u;
             const int r = c / QR, kq = 4 * (c % QR);
             const int d = m0 + r;
+            if constexpr (BUF) {
+                const uint32_t ox = d < D && kb + kq < K ? (uint32_t)((((long long)d * H + h) * K + kb + kq) * 4)
+                                                         : 0xFFFFFF00u;
+                rx[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, (int)ox, 0, 0));
+                if (!kind2) {
+                    const int w1 = n0 + r;
+                    fold_buf(prow0 + w1, kb + kq, w1 < W1, ry[u]);
+                } else {
+                    const int w1 = kb + (c >> 5);
+                    fold_buf(prow0 + w1, n0 + 4 * (c & 31), w1 < W1, ry[u]);
+                }
+                continue;
+            }
             const float *xrow = X + ((long long)(b * D + (d < D ? d : 0)) * H + h) * K;
             rx[u] = load_x_quad<VEC>(xrow, kb + kq, K, d < D);
             if (!kind2) {
@@ -979,7 +1020,11 @@ hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a_in, hipStream_t s) {
     // 2-level gradients; 3+ per-level layouts and odd widths keep the exact
     // kernel)
     const bool pairfold = a.nlev == 3 && a.g[1] == nullptr;
-    if (!a.exact && vec && (pairfold || a.nlev == 1 || a.nlev == 2)) {
+    const long long Prow = (long long)a.B * a.H * a.W1;
+    const bool fits = (long long)a.D * a.H * (a.W1 > a.W2 ? a.W1 : a.W2) * 4 < 0xFFFFFF00LL &&
+                      (Prow * a.ld[0] + a.shadow[0]) * 4 < 0xFFFFFF00LL &&
+                      (!pairfold || (Prow * a.ld[2] + a.shadow[2]) * 4 < 0xFFFFFF00LL);
+    if (!a.exact && vec && fits && (pairfold || a.nlev == 1 || a.nlev == 2)) {
 #ifdef RAFTCORR_DEV
         if (pairfold && rc::dev_knob("RAFTCORR_VBWD_VARIANT") == 2) {   // dev A/B: G^T staged by scattered loads
             hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, rc::kPairFold, false>), grid, blk, 0, s, a, (int)nwg);
