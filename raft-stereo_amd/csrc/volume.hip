@@ -973,12 +973,13 @@ static int device_cus() {
 }
 
 template <int NWN, int FMA, int SL, int MODE, bool DEFER>
-static void launch_bf16_ring_n(const BuildArgs &a, hipStream_t s) {
+static void launch_bf16_ring_n(const BuildArgs &a, hipStream_t s, int per_cu = 1) {
     constexpr int TW = B16Geom<NWN, FMA>::TW;
     const int tiles_m = (a.W1 + 127) / 128, tiles_n = (a.W2 + TW - 1) / TW;
     const long long ntiles = (long long)a.B * a.H * tiles_m * tiles_n;
     if (ntiles <= 0 || ntiles > 0x7FFFFFFF) return;
-    const long long nwg = ntiles < device_cus() ? ntiles : device_cus();   // one per CU (LDS-bound)
+    const long long cap = (long long)device_cus() * per_cu;                 // resident workgroups (LDS-bound)
+    const long long nwg = ntiles < cap ? ntiles : cap;
     // up to 3 fused levels (the default pair layout) keeps the epilogue's
     // level pointers out of the scalar registers the K loop needs
     if (DEFER || a.nfused <= 3)
@@ -988,6 +989,16 @@ static void launch_bf16_ring_n(const BuildArgs &a, hipStream_t s) {
         hipLaunchKernelGGL((build_bf16_ring_kernel<NWN, FMA, SL, MODE, kB16MaxFused, DEFER>), dim3((unsigned)nwg),
                            dim3(128 * NWN + 128), 0, s, a, (int)ntiles, tiles_m, tiles_n);
 }
+
+#ifdef RAFTCORR_DEV
+// dev: the 6-wave shape (128-wide w2 tiles, 75 / 65 KB of LDS) resident
+// twice per CU, so two independent barrier chains share each CU
+template <int MODE>
+static void launch_bf16_ring_two(const BuildArgs &a, bool defer, int per_cu, hipStream_t s) {
+    if (defer) launch_bf16_ring_n<2, 4, 4, MODE, true>(a, s, per_cu);
+    else launch_bf16_ring_n<2, 4, 3, MODE, false>(a, s, per_cu);
+}
+#endif
 
 // the deferred-epilogue kernel has no staging area: 4 ring slots
 template <int MODE>
@@ -1199,6 +1210,12 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
     // neither, 48 16-B-aligned (wrong) DMA sources
     const int mode = rc::dev_knob("RAFTCORR_BUILD_MODE");
     if (mode == 32) sh = rc::B16Shape{0, 0, false};
+    if (sh.nwn && (mode == 49 || mode == 50 || mode == 51)) {   // 6-wave shape: 2 / 1 per CU; 51: 2, no stores
+        if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
+        if (mode == 51) rc::launch_bf16_ring_two<2>(a, sh.defer, 2, s);
+        else rc::launch_bf16_ring_two<0>(a, sh.defer, mode == 49 ? 2 : 1, s);
+        return hipGetLastError();
+    }
     if (sh.nwn && mode >= 40 && mode <= 48) {
         if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
         switch (mode) {

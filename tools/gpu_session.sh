@@ -39,6 +39,7 @@ has ablatek && step ablate_kitti 600 python tools/ablate.py --config kitti --bui
 has configs && step bench_realtime 300 python bench.py --config realtime --no-cpu-baseline --steps 50 --warmup 5 && step bench_realtime_graph 300 python bench.py --config realtime --graph --no-cpu-baseline --steps 200 --warmup 10
 has configs && step bench_middlebury 300 python bench.py --config middlebury --no-cpu-baseline --steps 5 --warmup 2
 has configs && step bench_kitti 300 python bench.py --config kitti --no-cpu-baseline --steps 10 --warmup 3
+has ab16 && step ablate_b16 600 python tools/ablate.py --config kitti --build-modes ${AB16_MODES:-0,49,50,40,51} --lookup-variants 0 --rounds 5
 has kitti && step bench_kitti 300 python bench.py --config kitti --no-cpu-baseline --steps 10 --warmup 3
 if has profk; then
     step rocprof_kitti 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profk" -o trace \
