@@ -841,7 +841,8 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
     // whole 128-B row segments, 16 B per lane -- 8-B stores straight from
     // the registers would write each line in four pieces at different times
     // (measured 1.5x the HBM write bytes)
-    auto store_piece = [&](int nb) {
+    // halves [h0b, h1b) of piece nb: half 0 also stages the piece in LDS
+    auto store_piece = [&](int nb, int h0b = 0, int h1b = 2) {
         if (!hact) return;
         // opaque per piece, so that the addresses of all pieces are not
         // precomputed per tile and kept live through the K loop
@@ -849,13 +850,15 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
         asm volatile("" : "+v"(ln));
         const int g = ln >> 4, i16 = ln & 15;
         char *img = smem + SL * G::SLOT + wave * kB16DeferStage;
+        if (h0b == 0) {
 #pragma unroll
-        for (int ma = 0; ma < FMA; ++ma)
-            *reinterpret_cast<uint2 *>(img + i16 * 144 + (16 * ma + 4 * g) * 2) = uint2{h0[ma][nb][0], h0[ma][nb][1]};
+            for (int ma = 0; ma < FMA; ++ma)
+                *reinterpret_cast<uint2 *>(img + i16 * 144 + (16 * ma + 4 * g) * 2) =
+                    uint2{h0[ma][nb][0], h0[ma][nb][1]};
+        }
         uint16_t *l0 = reinterpret_cast<uint16_t *>(a.lvl[0]);
         const long long rowbase = (long long)hrow * W1;
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
+        for (int half = h0b; half < h1b; ++half) {
             const int R = 8 * half + (ln >> 3), c = ln & 7;
             const uint4 x = *reinterpret_cast<const uint4 *>(img + R * 144 + 16 * c);
             const int w1 = hm0 + 16 * nb + R, col = hn0 + 8 * c;
@@ -906,9 +909,20 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
         }
         if constexpr (DEFER && !(MODE & kModeNoStores)) {
             if (held) {
+                if constexpr ((MODE & kModeSpread) != 0) {   // 8 half-pieces, one per stage at nst = 8
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb)
-                    if (((nb * nst) >> 2) == st) store_piece(nb);
+                    for (int p = 0; p < 8; ++p)
+                        if (((p * nst) >> 3) == st) store_piece(p >> 1, p & 1, (p & 1) + 1);
+                } else if constexpr ((MODE & kModeStagger) != 0) {   // odd waves one stage later
+                    const int off = nst >= 8 ? (wave & 1) : 0;
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        if (((nb * nst) >> 2) + off == st) store_piece(nb);
+                } else {
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        if (((nb * nst) >> 2) == st) store_piece(nb);
+                }
             }
         }
         if (++st == nst) {
@@ -1210,6 +1224,12 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
     // neither, 48 16-B-aligned (wrong) DMA sources
     const int mode = rc::dev_knob("RAFTCORR_BUILD_MODE");
     if (mode == 32) sh = rc::B16Shape{0, 0, false};
+    if (sh.nwn && (mode == 52 || mode == 53)) {   // stores spread over 8 stages / staggered by wave parity
+        if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
+        if (mode == 52) rc::launch_bf16_ring<rc::kModeSpread>(a, sh, s);
+        else rc::launch_bf16_ring<rc::kModeStagger>(a, sh, s);
+        return hipGetLastError();
+    }
     if (sh.nwn && (mode == 49 || mode == 50 || mode == 51)) {   // 6-wave shape: 2 / 1 per CU; 51: 2, no stores
         if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
         if (mode == 51) rc::launch_bf16_ring_two<2>(a, sh.defer, 2, s);
