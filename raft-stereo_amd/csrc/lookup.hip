@@ -500,6 +500,125 @@ __device__ __forceinline__ void tap_span(float xl, int W, int &f, int &l) {
     l = min((int)floorf(pb) + 1, W - 1);
 }
 
+#ifdef RAFTCORR_DEV
+// Level-0 chain (dev variant 220): every level 0..NL-1
+// derived from ONE span of level 0 -- the top level's 2r+4 window scaled by
+// S = 2^(NL-1) (96 elements at L = 4, r = 4), exact-span predicated -- so the
+// lookups read level 0 only (249 MB at config 2 instead of levels 0 + 2 and the
+// level-2 copy) at the cost of more 64-B sectors per pixel (4.7 vs 3.7
+// simulated).  Level i window element jj is the pool_tree of 2^i level-0
+// elements, the fp32 ops of avg_pool2d applied i times (model.py:294).
+template <int R, int NL>
+__global__ __launch_bounds__(256) void lookup_l0chain_kernel(LookupArgs a) {
+    constexpr int T = 2 * R + 1, NW = 2 * R + 4, TOP = NL - 1, S = 1 << TOP;
+    constexpr int NE0 = S * NW, NC0 = NE0 / 4;
+    static_assert(S % 4 == 0, "span start must be 16-B aligned");
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const long long pblk = (long long)blk * 256;
+    const long long p = pblk + threadIdx.x;
+    const bool active = p < a.P;
+    const long long pp = active ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    const float x = pixel_x(a, bimg, rem, active);
+    float *outp = a.out + bimg * (long long)(NL * T) * a.HW + rem;
+    const long long lrow = pp - pblk;
+    const float xtop = x / (float)(1 << TOP);
+    const bool inwin = (xtop > -(float)(R + 4)) && (xtop < (float)(a.W[TOP] + R + 4));
+    const float ntop = inwin ? floorf(xtop) : 0.0f;
+    const int e0 = S * ((int)ntop - R - 1);
+    int lo = 0x7FFFFFFF, hi = -1;
+    if (inwin) {
+#pragma unroll
+        for (int i = 0; i <= TOP; ++i) {
+            int f, l;
+            tap_span<R>(x / (float)(1 << i), a.W[i], f, l);
+            if (f <= l) {
+                lo = min(lo, f << i);
+                hi = max(hi, ((l + 1) << i) - 1);
+            }
+        }
+    }
+    const long long ld0 = a.ld[0];
+    const float *lvl0 = static_cast<const float *>(a.lvl[0]);
+    const auto rs0 = make_rsrc(lvl0 + pblk * ld0, clamp_bytes((a.P - pblk) * ld0 * 4));
+    float s0[NE0];
+#pragma unroll
+    for (int k = 0; k < NC0; ++k) {
+        const int cs = e0 + 4 * k;
+        const bool ok = cs <= hi && cs + 3 >= lo;
+        const f32x4 v = ld4(rs0, ok ? (uint32_t)((lrow * ld0 + cs) * 4) : 0xFFFFFF00u);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s0[4 * k + c] = v[c];
+    }
+    const float *row0 = lvl0 + pp * ld0;
+    auto level = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int SI = 1 << i, NDD = 1 << (TOP - i);
+        const int W = a.W[i];
+        const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
+        const DivRN dv = div_prep(Wm1);
+        const float xl = x / (float)(1 << i);
+        const float n = inwin ? floorf(xl) : 0.0f;
+        const int dd = inwin ? (int)n - NDD * (int)ntop : 0;
+        const bool valid = inwin && dd >= 0 && dd < NDD;
+        float w[NW];
+#pragma unroll
+        for (int jj = 0; jj < NW; ++jj) {
+            float val = 0.0f;
+#pragma unroll
+            for (int d = 0; d < NDD; ++d) {
+                constexpr int base = (R + 1) * (S - SI);
+                const float v = pool_tree<SI>(s0 + base + SI * (d + jj));
+                val = (dd == d) ? v : val;
+            }
+            w[jj] = val;
+        }
+        float res[T];
+        bool bad = false;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + xl;
+            const float xn = div_rn(2.0f * xt, dv) - 1.0f;
+            const float xp = (xn + 1.0f) * half;
+            const float x0 = floorf(xp);
+            const float w1 = xp - x0, w0 = 1.0f - w1;
+            const float nt = n + (float)(t - R);
+            const bool lo_ = x0 < nt, hi_ = x0 > nt;
+            float e0_ = w[t], e1_ = w[t + 1], e2_ = w[t + 2], e3_ = w[t + 3];
+            asm("" : "+v"(e0_), "+v"(e1_), "+v"(e2_), "+v"(e3_));
+            const float a0 = lo_ ? e0_ : (hi_ ? e2_ : e1_);
+            const float a1 = lo_ ? e1_ : (hi_ ? e3_ : e2_);
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            bad |= inwin && (!valid || x0 < nt - 1.0f || x0 > nt + 1.0f);
+            res[t] = fmaf(w1, ok1 ? a1 : 0.0f, w0 * (ok0 ? a0 : 0.0f));
+        }
+        if (__builtin_expect(bad, 0)) {
+            for (int t = 0; t < T; ++t) {
+                const float xt = (float)(t - R) + xl;
+                const float xn = div_rn(2.0f * xt, dv) - 1.0f;
+                const float xp = (xn + 1.0f) * half;
+                const float x0 = floorf(xp);
+                const float w1 = xp - x0, w0 = 1.0f - w1;
+                const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+                const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+                const float v0 = ok0 ? derived_elem<SI>(row0, (long long)x0) : 0.0f;
+                const float v1 = ok1 ? derived_elem<SI>(row0, (long long)x0 + 1) : 0.0f;
+                res[t] = fmaf(w1, v1, w0 * v0);
+            }
+        }
+        if (active) {
+#pragma unroll
+            for (int t = 0; t < T; ++t) outp[(long long)(i * T + t) * a.HW] = res[t];
+        }
+    };
+    level(std::integral_constant<int, 0>{});
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    if constexpr (TOP >= 3) level(std::integral_constant<int, 3>{});
+}
+#endif
+
 // PH (dev-only timing probes; the values read are NOT the span's): 1 = read
 // each span at +64 B when that touches fewer 128-B lines (what a second,
 // half-line-shifted copy of the level would give), 2 = move every span to a
@@ -773,6 +892,106 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// Persistent pair lookup (dev variants 215-219 while measured).  The one-round
+// grid of lookup_pair_kernel puts every wave in the same phase: all spans are
+// requested at launch and each wave's output stores follow its own loads.
+// Here each wave walks 64-pixel groups g, g + S, g + 2S, ... of its XCD's
+// contiguous share of the image (S = waves on that XCD), and with PIPE the
+// spans of group n+1 are requested before group n's tap math and stores, so a
+// wave's stores overlap its own next loads; the x of group n+2 is loaded one
+// stage ahead, so issuing the next spans never waits on the current ones.
+// Same PairSpan / finish_pair as the pair kernel: bit-identical output.
+__device__ __forceinline__ float group_x(const LookupArgs &a, long long g, int lane) {
+    const long long p = g * 64 + lane;
+    const long long pp = p < a.P ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    return pixel_x(a, bimg, rem, p < a.P);
+}
+
+template <int R, int NL, bool BF16, bool PIPE, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_pair_persist_kernel(LookupArgs a) {
+    static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
+    constexpr int NP = NL / 2;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const long long NG = (a.P + 63) >> 6;
+    const int nb = gridDim.x, xcd = blockIdx.x & 7, kb = blockIdx.x >> 3;
+    const int nbx = (nb >> 3) + (xcd < (nb & 7) ? 1 : 0);          // blocks on this XCD
+    const long long gq = NG >> 3, gr = NG & 7;
+    const long long g0 = xcd * gq + (xcd < gr ? xcd : gr);
+    const long long g1 = g0 + gq + (xcd < gr ? 1 : 0);              // this XCD's groups [g0, g1)
+    const long long S = 4LL * nbx;
+    long long g = g0 + 4LL * kb + w;
+    if (g >= g1) return;
+    auto pix = [&](long long gg, float x) {
+        PairPixel q;
+        q.pblk = gg * 64;
+        const long long p = q.pblk + lane;
+        q.active = p < a.P;
+        q.pp = q.active ? p : a.P - 1;
+        const long long bimg = q.pp / a.HW, rem = q.pp - bimg * a.HW;
+        q.x = x;
+        q.outp = a.out + bimg * (long long)(NL * (2 * R + 1)) * a.HW + rem;
+        q.lrow = lane;
+        return q;
+    };
+    auto sink_of = [&](const PairPixel &q) {
+        return [&a, q](int ch, float v) {
+            if (q.active) q.outp[(long long)ch * a.HW] = v;
+        };
+    };
+    if constexpr (!PIPE) {
+        for (; g < g1; g += S) {
+            const PairPixel q = pix(g, group_x(a, g, lane));
+            PairSpan<R, BF16> sp[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
+#pragma unroll
+            for (int k = 0; k < NP; ++k) finish_pair<R, false, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink_of(q));
+        }
+    } else {
+        PairPixel qa = pix(g, group_x(a, g, lane));
+        float xn = g + S < g1 ? group_x(a, g + S, lane) : 0.0f;   // x of the next group
+        PairSpan<R, BF16> sa[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sa[k], a, 2 * k, qa.x, qa.pblk, qa.lrow);
+        for (;;) {
+            const long long gn = g + S;
+            const bool more = gn < g1;                               // wave-uniform
+            PairPixel qb;
+            PairSpan<R, BF16> sb[NP];
+            if (more) {
+                const float x2 = gn + S < g1 ? group_x(a, gn + S, lane) : 0.0f;
+                qb = pix(gn, xn);
+#pragma unroll
+                for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sb[k], a, 2 * k, qb.x, qb.pblk, qb.lrow);
+                xn = x2;
+            }
+#pragma unroll
+            for (int k = 0; k < NP; ++k) finish_pair<R, false, BF16>(sa[k], a, 2 * k, qa.x, qa.pp, sink_of(qa));
+            if (!more) break;
+            qa = qb;
+#pragma unroll
+            for (int k = 0; k < NP; ++k) sa[k] = sb[k];
+            g = gn;
+        }
+    }
+}
+
+template <int R, bool PIPE, int WPE>
+static void launch_pair_persist(const LookupArgs &a, int bf16, int blocks_per_cu, hipStream_t s) {
+    const long long NG = (a.P + 63) >> 6;
+    long long nblk = 256LL * blocks_per_cu;                         // MI355X: 256 CUs
+    if (nblk * 4 > NG) nblk = (NG + 3) / 4;
+    if (a.levels == 4) {
+        if (bf16) hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 4, true, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 4, false, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
+    } else {
+        if (bf16) hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 2, true, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 2, false, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
+    }
+}
+
 // Cooperative span loads (dev variants 212-214 while measured).  The pair
 // kernel above has each lane fetch its own two spans with 7 (fp32) 16-B
 // loads: every wave-instruction then touches 64 different rows, and a span's
@@ -993,6 +1212,19 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
             if (v == 212) launch_pair_coop<R, 1>(a, bf16, s);
             if (v == 213) launch_pair_coop<R, 2>(a, bf16, s);
             if (v == 214) launch_pair_coop<R, 4>(a, bf16, s);
+            return hipGetLastError();
+        }
+        // persistent pair lookup: 215 = one group at a time, 2 blocks/CU;
+        // 216 / 217 = pipelined, 1 / 2 blocks per CU (more spill to scratch)
+        if ((a.levels == 4 || a.levels == 2) && !a.out_cl && v >= 215 && v <= 217) {
+            if (v == 215) launch_pair_persist<R, false, 2>(a, bf16, 2, s);
+            if (v == 216) launch_pair_persist<R, true, 1>(a, bf16, 1, s);
+            if (v == 217) launch_pair_persist<R, true, 2>(a, bf16, 2, s);
+            return hipGetLastError();
+        }
+        // 220: level-0 chain (reads level 0 only; fp32, 4 levels)
+        if (a.levels == 4 && !bf16 && !a.out_cl && v == 220) {
+            hipLaunchKernelGGL((lookup_l0chain_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
             return hipGetLastError();
         }
         if (a.levels == 4 && v == 210 && a.dbg) {

@@ -91,6 +91,17 @@ if has pmcv; then
         --output-format csv -d "$OUT/pmc_v2" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
     python tools/pmc_raw.py "$OUT/pmc_v1" > "$OUT/pmc_v.txt" 2>&1; python tools/pmc_raw.py "$OUT/pmc_v2" >> "$OUT/pmc_v.txt" 2>&1; cat "$OUT/pmc_v.txt"
 fi
+if has pmcl; then   # lookup variants: L1->L2 request count / latency, L2 hits, fabric request sizes
+    step pmc_l1 120 rocprofv3 --pmc TCP_TCC_READ_REQ_LATENCY TCP_TCC_READ_REQ TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES GRBM_GUI_ACTIVE \
+        --output-format csv -d "$OUT/pmc_l1" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
+    step pmc_l2 120 rocprofv3 --pmc TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B TCC_HIT TCC_MISS \
+        --output-format csv -d "$OUT/pmc_l2" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
+    step pmc_l3 120 rocprofv3 --pmc TCC_EA0_RDREQ_LEVEL TCC_EA0_RDREQ TCC_EA0_RDREQ_DRAM_CREDIT_STALL TCC_EA0_WRREQ \
+        --output-format csv -d "$OUT/pmc_l3" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
+    { python tools/pmc_raw.py "$OUT/pmc_l1" --width 90; python tools/pmc_raw.py "$OUT/pmc_l2" --width 90;
+      python tools/pmc_raw.py "$OUT/pmc_l3" --width 90; } > "$OUT/pmc_l.txt" 2>&1; grep lookup "$OUT/pmc_l.txt"
+fi
+has lprobe2 && step lookup_probe2 600 python tools/lookup_probe.py --only-dev --dev-variants ${LPROBE_VARIANTS:-215} --dev-fields ${LPROBE_FIELDS:-bench,smooth,net} --reps ${LPROBE_REPS:-7}
 if has calib; then   # FETCH_SIZE / WRITE_SIZE per byte for scattered 64-256 B rows
     step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o f \
         -- python3 tools/pmc_calib_random.py
