@@ -440,6 +440,10 @@ def main():
                     help="force the reference's NCHW-contiguous lookup output")
     ap.add_argument("--no-backward", action="store_true",
                     help="skip the corr-path backward timing (sceneflow only)")
+    ap.add_argument("--per-rank-of", type=int, default=0,
+                    help="single-GPU projection input: run rank 0's share of an N-GPU job "
+                         "(kitti: batch 64/N; middlebury: H/N feature rows) and report the "
+                         "rate N such ranks would reach with no exchange (DESIGN.md §5)")
     args = ap.parse_args()
     if args.channels_last is None:   # NHWC output where it goes to HBM (the bf16 config)
         args.channels_last = args.config in BF16_CONFIGS
@@ -468,18 +472,20 @@ def main():
 
     cfg = CONFIGS[args.config]
     global_batch = args.config in GLOBAL_BATCH_CONFIGS
+    proj = args.per_rank_of if world == 1 and args.per_rank_of > 1 else 0
+    split_world = proj or world                    # ranks the job's work is cut into
     if global_batch:
         from raft_stereo_amd.shard import split_range
-        b0, b1 = split_range(cfg[0], rank, world)
+        b0, b1 = split_range(cfg[0], rank, split_world)
         cfg = (b1 - b0,) + cfg[1:]
     B, D, H, W1, W2, L, r, iters, desc = cfg
     bf16 = args.config in BF16_CONFIGS
-    row_shard = args.config in ROW_SHARD_CONFIGS and world > 1
+    row_shard = args.config in ROW_SHARD_CONFIGS and split_world > 1
     if row_shard:
         # config 4: ONE full-resolution pair, image rows sharded over ranks
         # (strong scaling); the corr path is row-local, so no exchange.
         from raft_stereo_amd.shard import split_range
-        r0, r1 = split_range(H, rank, world)
+        r0, r1 = split_range(H, rank, split_world)
         f1, f2, coords = make_inputs(cfg, device, seed=1)
         f1 = f1[:, :, r0:r1].contiguous()
         f2 = f2[:, :, r0:r1].contiguous()
@@ -541,18 +547,26 @@ def main():
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
-        build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        build_in_loop_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
         lookup_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps / iters
 
-        if args.graph:   # a replay has no per-kernel events: time eager builds instead
-            be = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(5)]
-            for e0, e1 in be:
-                e0.record()
-                CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
-                            low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
-                e1.record()
+        # Build duration without host time: a device-side sleep first, so the
+        # host has queued the whole CorrBlock1D construction (allocations,
+        # validation, the build launch) before the GPU reaches the first event
+        # -- at small sizes (realtime) the event pair otherwise spans the host
+        # gap in front of the launch.  Median of 7.
+        bl = []
+        for _ in range(7):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(5_000_000)
+            e0.record()
+            CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
+                        low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
+            e1.record()
             torch.cuda.synchronize()
-            build_ms = sum(e0.elapsed_time(e1) for e0, e1 in be) / len(be)
+            bl.append(e0.elapsed_time(e1))
+        bl.sort()
+        build_ms = bl[len(bl) // 2]
         # per-launch lookup duration without the host gaps between launches:
         # events around each launch of one extra pass
         # A device-side sleep first lets the host queue every launch before the
@@ -684,7 +698,8 @@ def main():
         "roofline_lookup": roof_lookup,
         "lookup_gbs": lgbs,
         "latency_ms": {"p50": lat[len(lat) // 2], "min": lat[0], "max": lat[-1]},
-        "kernel_ms": {"build": build_ms, "lookup_in_loop": lookup_ms,
+        "kernel_ms": {"build": build_ms, "build_in_loop": None if args.graph else build_in_loop_ms,
+                      "lookup_in_loop": lookup_ms,
                       "lookup_per_launch": lookup_launch_ms},
         "cpu_baseline": None,
         "notes": (f"pool-chain block: the build writes pyramid levels {written} (levels "
@@ -725,6 +740,17 @@ def main():
             "unfused": e2e_pairs_per_s(cfg, device, max(args.e2e_steps, 10), 3, (480, 640)),
             "fused_step": e2e_pairs_per_s(cfg, device, max(args.e2e_steps, 10), 3, (480, 640),
                                           fuse_step=True)}
+    if proj:
+        # one GPU ran rank 0's share of a proj-GPU job: the rate proj such
+        # ranks reach when nothing is exchanged (batch shards; the corr path of
+        # row shards).  A projection from measured per-rank work, not a
+        # multi-GPU measurement.
+        result["projection"] = {
+            "per_rank_of": proj, "rank_share": ({"rows": [r0, r1]} if row_shard else {"batch": B}),
+            "projected_ms_per_step": ms_per_step,
+            "projected_value": job_pairs / (ms_per_step * 1e-3),
+            "note": "single GPU timing rank 0's share; no collective in the timed path"}
+        result["config"]["parallelism"] = f"rank 0 of {proj} (single-GPU projection input)"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds,
                                               full=args.config == "sceneflow")

@@ -219,13 +219,17 @@ int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths, const long
  * arguments as in rc_corr_lookup_backward (all calls share B, H, W1, levels,
  * radius).  levels | RC_GRAD_OVERWRITE: the buffers receive the sum instead
  * of having it added (they need not be zeroed first; row padding up to the
- * next multiple of 4 columns is written as zeros).  With the pair layout and
- * level-0 rows of at most ~1.5K floats at r = 4 the pixel's rows stay on chip
- * while all calls accumulate, so each call's inputs are read once and each
- * row written once; otherwise, and for the per-level
- * layout, this is a loop over rc_corr_lookup_backward.  RC_SHADOW_LEVEL bits
- * are RC_EUNSUPPORTED here.  RC_GRAD_OVERWRITE with n_calls == 0 is
- * RC_EINVAL; n_calls == 0 otherwise does nothing. */
+ * next multiple of 4 columns is written as zeros).  With the pair layout each
+ * lane keeps the union of its calls' windows of its pixel's rows on chip
+ * (compact rows: any level-0 width whose LDS budget max(5120, 2(W + 8r + 24))
+ * floats fits 64 KB, i.e. W up to about 8K), so each call's inputs are read
+ * once and each row written once, in launches of up to 32
+ * calls.  Wider rows, per-call coords or grad_out extents past the kernel's
+ * 32-bit offsets, and the per-level layout run a loop over
+ * rc_corr_lookup_backward instead -- chosen for the whole request before the
+ * first launch.  RC_SHADOW_LEVEL bits are RC_EUNSUPPORTED here; other flag
+ * bits than RC_GRAD_OVERWRITE are RC_EINVAL.  RC_GRAD_OVERWRITE with
+ * n_calls == 0 is RC_EINVAL; n_calls == 0 otherwise does nothing. */
 #define RC_GRAD_OVERWRITE 0x40000
 int rc_corr_lookup_backward_calls(void *const *grad_pyr, const int *widths, const long *grad_ld,
                                   int levels, int radius, int n_calls,

@@ -530,7 +530,18 @@ class _GradState:
     record their (coords, grad_out); the build node sums all of them in one
     rc_corr_lookup_backward_calls pass (``deferred``) into
     buffers it never zeroes.  Otherwise each lookup node adds its call into
-    zeroed buffers right away (rc_corr_lookup_backward)."""
+    zeroed buffers right away (rc_corr_lookup_backward).
+
+    Retention: a recorded grad_out is converted to contiguous
+    fp32 when it is recorded (one copy alive, not a second one per call at the
+    end), and once ``max_pending_calls`` calls (one kernel launch's worth) or
+    ``max_pending_bytes`` of them are pending they are summed right away -- the
+    first partial pass overwrites the buffers, later ones add -- so at most
+    that much is held however many iterations run.  Config 2 holds 32 x 37 MB
+    (= 1.19 GB) until the build node, DESIGN.md §3.4c."""
+
+    max_pending_calls = 32             # kMaxBwdCalls: the calls of one kernel launch
+    max_pending_bytes = 2 << 30
 
     def __init__(self, P, widths, device, num_levels, radius, grad_shadow=None, deferred=None,
                  exact_f32=False):
@@ -546,6 +557,7 @@ class _GradState:
         self.deferred = bool(deferred) and self.pair and not self.grad_shadow
         self.grads = None
         self.pending = []
+        self.pending_bytes = 0
         self.token_sent = False
 
     def token_grad(self, device):
@@ -556,20 +568,31 @@ class _GradState:
 
     def accumulate(self, coords, grad_out):
         if self.deferred:
-            self.pending.append((coords, grad_out))
+            go = grad_out.detach().float().contiguous()
+            self.pending.append((coords, go))
+            self.pending_bytes += go.numel() * go.element_size()
+            if (len(self.pending) >= self.max_pending_calls
+                    or self.pending_bytes >= self.max_pending_bytes):
+                self._flush()
             return
         if self.grads is None:
             self.grads = grad_buffers(self.P, self.widths, self.device, pair=self.pair,
                                       shadow=self.grad_shadow)
         lookup_backward(self.grads, coords, grad_out, self.num_levels, self.radius)
 
+    def _flush(self):
+        """Sum the pending calls: into fresh (unzeroed) buffers the first time
+        (RC_GRAD_OVERWRITE), added to them afterwards."""
+        calls, self.pending, self.pending_bytes = self.pending, [], 0
+        first = self.grads is None
+        if first:
+            self.grads = grad_buffers(self.P, self.widths, self.device, pair=True, zero=False)
+        lookup_backward_calls(self.grads, [c for c, _ in calls], [g for _, g in calls],
+                              self.num_levels, self.radius, overwrite=first)
+
     def take(self):
         if self.pending:
-            calls, self.pending = self.pending, []
-            grads = grad_buffers(self.P, self.widths, self.device, pair=True, zero=False)
-            lookup_backward_calls(grads, [c for c, _ in calls], [g for _, g in calls],
-                                  self.num_levels, self.radius, overwrite=True)
-            return grads
+            self._flush()
         g, self.grads = self.grads, None
         return g
 

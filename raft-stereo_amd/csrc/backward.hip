@@ -797,9 +797,12 @@ __device__ __forceinline__ void volume_bwd_split_tile(const BuildBwdArgs &a, flo
                 if (!kind2) {
                     const int w1 = n0 + r;
                     fold_buf(prow0 + w1, kb + kq, w1 < W1, ry[u]);
-                } else {
+                } else if constexpr (KM) {            // G rows, coalesced along w2
                     const int w1 = kb + (c >> 5);
                     fold_buf(prow0 + w1, n0 + 4 * (c & 31), w1 < W1, ry[u]);
+                } else {                              // the mapping write_stage's !KM branch reads
+                    const int w1 = kb + (c % kBwdK);
+                    fold_buf(prow0 + w1, n0 + 4 * (c / kBwdK), w1 < W1, ry[u]);
                 }
                 continue;
             }

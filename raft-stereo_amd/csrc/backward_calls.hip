@@ -505,6 +505,28 @@ __global__ __launch_bounds__(64) void lookup_bwd_calls_compact_kernel(LookupBwdC
 // LDS per workgroup: pair k holds pix rows of S_k = round4(W_2k) + M floats
 // after a leading margin M = 4r+4 (the strips' reach past either end of a
 // row); pix is the largest of 64/(NL/2), ..., 8 pixels whose rows fit 64 KB.
+// Whether the fused kernels serve a whole request of n_calls calls (coords
+// batch strides cbs[0..n_calls)) on a.P / a.HW / a.W: the per-call buffer
+// resources address each output gradient and coords tensor with 32-bit
+// offsets, and a block's rows must fit 64 KB of LDS (compact rows, else whole
+// rows).  rc_corr_lookup_backward_calls asks this once, before any launch,
+// and otherwise takes the per-call path for the whole request.
+bool rc_lookup_bwd_calls_fits(const rc::LookupBwdCallsArgs &a, int radius, int levels, const long *cbs,
+                              int n_calls) {
+    if ((levels != 2 && levels != 4) || radius < 1 || radius > 4) return false;
+    if (a.P * levels * (2 * radius + 1) * 4 >= 0xFFFFFF00LL) return false;
+    for (int c = 0; c < n_calls; ++c)
+        if (((a.P / a.HW - 1) * (long long)cbs[c] + a.HW) * 4 >= 0xFFFFFF00LL) return false;
+    const int np = levels / 2, M = 4 * radius + 4;
+    int maxS = 0, per_pix = 0;
+    for (int k = 0; k < np; ++k) {
+        maxS = std::max(maxS, ((a.W[2 * k] + 8 * radius + 24) + 3) & ~3);
+        per_pix += ((a.W[2 * k] + 3) & ~3) + M;
+    }
+    if ((long long)std::max(5120, 2 * maxS) * 4 <= 65536) return true;     // compact rows
+    return (long long)(per_pix * 8 + np * M) * 4 <= 65536;                 // whole rows, 8 pixels
+}
+
 hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int levels, hipStream_t s) {
     if (a.P <= 0 || a.ncalls <= 0) return hipSuccess;
     if (a.ncalls > rc::kMaxBwdCalls || (levels != 2 && levels != 4) || radius < 1 || radius > 4)

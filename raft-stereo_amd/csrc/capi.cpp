@@ -428,6 +428,8 @@ extern "C" int rc_corr_lookup_backward(void *const *grad_pyr, const int *widths,
                                        const float *coords_x, long coord_batch_stride, int B,
                                        int H, int W1, const float *grad_out, void *stream) {
     g_err[0] = 0;
+    if (levels & ~0xFFFF)
+        return fail(RC_EINVAL, "rc_corr_lookup_backward: unknown flag bits 0x%x", levels & ~0xFFFF);
     rc::LookupBwdArgs a;
     bool empty = false, pair = false;
     int rc = prep_lookup_bwd("rc_corr_lookup_backward", grad_pyr, widths, grad_ld, levels, radius,
@@ -446,6 +448,7 @@ extern "C" int rc_corr_lookup_backward_calls(void *const *grad_pyr, const int *w
     const char *who = "rc_corr_lookup_backward_calls";
     const bool overwrite = (levels & RC_GRAD_OVERWRITE) != 0;
     levels &= ~RC_GRAD_OVERWRITE;
+    if (levels & ~0xFFFF) return fail(RC_EINVAL, "%s: unknown flag bits 0x%x", who, levels & ~0xFFFF);
     if (n_calls < 0) return fail(RC_EINVAL, "%s: n_calls=%d", who, n_calls);
     if (n_calls > 0 && (!coords_x || !coord_batch_stride || !grad_out))
         return fail(RC_EINVAL, "%s: null coords / stride / grad_out array", who);
@@ -491,6 +494,8 @@ extern "C" int rc_corr_lookup_backward_calls(void *const *grad_pyr, const int *w
     for (int i = 0; i < a.levels; ++i) ca.W[i] = a.W[i];
     ca.P = a.P;
     ca.HW = a.HW;
+    // fused or per-call for the WHOLE request, decided before any launch
+    if (!rc_lookup_bwd_calls_fits(ca, radius, a.levels, coord_batch_stride, n_calls)) return per_call();
     for (int c0 = 0; c0 < n_calls; c0 += rc::kMaxBwdCalls) {
         ca.ncalls = std::min(rc::kMaxBwdCalls, n_calls - c0);
         ca.accumulate = (c0 > 0 || !overwrite) ? 1 : 0;
@@ -500,7 +505,6 @@ extern "C" int rc_corr_lookup_backward_calls(void *const *grad_pyr, const int *w
             ca.grad_out[c] = grad_out[c0 + c];
         }
         hipError_t e = rc_launch_lookup_bwd_calls(ca, radius, a.levels, s);
-        if (e == hipErrorNotSupported && c0 == 0) return per_call();   // nothing launched yet
         if (e != hipSuccess) return hip_rc(e, "rc_corr_lookup_backward_calls: launch");
     }
     return RC_OK;

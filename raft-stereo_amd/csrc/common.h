@@ -199,6 +199,8 @@ hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, int pyr_bf
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s);
 // fills a.pix / rowbase / S / lds_floats from W, radius, levels
 hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int levels, hipStream_t s);
+bool rc_lookup_bwd_calls_fits(const rc::LookupBwdCallsArgs &a, int radius, int levels, const long *cbs,
+                              int n_calls);
 hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a, hipStream_t s);
 hipError_t rc_launch_convex_upsample(const float *flow, const float *mask, int N, int C, int H,
                                      int W, int factor, float *out, hipStream_t s);

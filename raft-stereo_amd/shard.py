@@ -13,6 +13,8 @@ strictly row-local -- row h of fmap1 only meets row h of fmap2
 again with no exchange.  ``RowShardedStereo`` runs the whole network that
 way, exchanging only the GRU state halos each iteration.
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -174,7 +176,7 @@ class RowShardedStereo:
     """
 
     def __init__(self, model, rank, world, halo=None, group=None, shard_encoders=True, enc_margin=48,
-                 per_stage=True, encoder_halos=True):
+                 per_stage=True, encoder_halos=True, overlap=True):
         # one stage's cone needs 12 rows; a whole iteration's up to 20
         if halo is None:
             halo = 12 if per_stage else 24
@@ -193,7 +195,17 @@ class RowShardedStereo:
         # (_features_halo); False: a band of enc_margin extra rows recomputed
         # locally (_features_rows)
         self.encoder_halos = encoder_halos
+        # overlap (default, per_stage only): every halo exchange is posted as
+        # soon as its rows are final and waited for only right before the first
+        # op that reads the halo; the independent work in between (the next
+        # GRU stage's inputs, the corr lookup, the motion encoder; the 1/8-res
+        # heads and conv2 during layer4's exchanges) runs while it is in flight
+        # (RCCL: on the comm stream).  Same ops on the same values: the result
+        # equals the blocking order bit for bit.
+        self.overlap = overlap
         self._fake_xchg = False     # tools/shard_probe.py: time one rank's compute alone
+        self.xchg_wait_s = 0.0      # host time spent blocked in exchange waits
+        self.xchg_count = 0
 
     # row geometry -----------------------------------------------------------
     def _ranges(self, H1):
@@ -217,33 +229,48 @@ class RowShardedStereo:
         bottom halo) and next my rows [max(r0, r1-h), r1) (its top halo); I
         receive [e0, r0) and [r1, e1).  Sizes agree because every rank but
         the last owns >= halo rows."""
+        return self._exchange_finish(self._exchange_start(t, l, own, ext, glob))
+
+    def _exchange_start(self, t, l, own, ext, glob):
+        """Post _exchange's sends and receives and return a handle for
+        _exchange_finish; ``t`` is only read (the sends are copies)."""
         if self.world == 1:
-            return t
+            return (t, None, [], False, t.device, [])
         (r0, r1), (e0, e1) = own, ext
         h = self.halo >> l
         dev = t.device
         staged = _host_staged(t, self.group)
         if staged:
             t = t.cpu()
-        ops, recv = [], []
+        ops, recv, sends = [], [], []
         prev, nxt = self.rank - 1, self.rank + 1
         if prev >= 0:
             buf = torch.empty_like(t[:, :, 0:r0 - e0]).contiguous()
             ops.append(dist.P2POp(dist.irecv, buf, prev, group=self.group))
             recv.append((buf, 0))
             hi = min(glob, r0 + h, r1)
-            ops.append(dist.P2POp(dist.isend, t[:, :, r0 - e0:hi - e0].contiguous(), prev,
-                                  group=self.group))
+            sends.append(t[:, :, r0 - e0:hi - e0].clone(memory_format=torch.contiguous_format))
+            ops.append(dist.P2POp(dist.isend, sends[-1], prev, group=self.group))
         if nxt < self.world:
             buf = torch.empty_like(t[:, :, r1 - e0:e1 - e0]).contiguous()
             ops.append(dist.P2POp(dist.irecv, buf, nxt, group=self.group))
             recv.append((buf, r1 - e0))
             lo = max(r0, r1 - h)
-            ops.append(dist.P2POp(dist.isend, t[:, :, lo - e0:r1 - e0].contiguous(), nxt,
-                                  group=self.group))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+            sends.append(t[:, :, lo - e0:r1 - e0].clone(memory_format=torch.contiguous_format))
+            ops.append(dist.P2POp(dist.isend, sends[-1], nxt, group=self.group))
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        return (t, reqs, recv, staged, dev, sends)
+
+    def _exchange_finish(self, hd):
+        """Wait for a posted exchange; the slab with its halo rows refreshed."""
+        t, reqs, recv, staged, dev, _sends = hd
+        if reqs is None:
+            return t
+        t0 = time.perf_counter()
+        for req in reqs:
+            req.wait()
+        self.xchg_wait_s += time.perf_counter() - t0
+        self.xchg_count += 1
         if recv:
             t = t.clone()
             for buf, at in recv:
@@ -308,29 +335,42 @@ class RowShardedStereo:
         rank's own rows [lo, hi) of a level of height Hg): the h rows on
         either side come from the neighbours' own boundary rows (every rank
         owns >= h rows of every level).  Returns (slab, first global row)."""
+        return self._halo_finish(self._halo_start(t, lo, hi, Hg, h))
+
+    def _halo_start(self, t, lo, hi, Hg, h):
+        """Post _halo's exchange; a handle for _halo_finish."""
         g0, g1 = max(0, lo - h), min(Hg, hi + h)
         if self.world == 1 or h == 0:
-            return t, lo
+            return ("done", t, lo)
         if self._fake_xchg:          # timing probe: same shapes, no communication
             top = t.new_zeros(t.shape[:2] + (lo - g0,) + t.shape[3:])
             bot = t.new_zeros(t.shape[:2] + (g1 - hi,) + t.shape[3:])
-            return torch.cat([top, t, bot], 2), g0
-        dev = t.device
+            return ("done", torch.cat([top, t, bot], 2), g0)
         staged = _host_staged(t, self.group)
         src = t.cpu() if staged else t
-        ops, top, bot = [], None, None
+        ops, top, bot, sends = [], None, None, []
         if lo > 0:
             top = torch.empty_like(src[:, :, :lo - g0]).contiguous()
+            sends.append(src[:, :, :min(h, hi - lo)].clone(memory_format=torch.contiguous_format))
             ops += [dist.P2POp(dist.irecv, top, self.rank - 1, group=self.group),
-                    dist.P2POp(dist.isend, src[:, :, :min(h, hi - lo)].contiguous(), self.rank - 1,
-                               group=self.group)]
+                    dist.P2POp(dist.isend, sends[-1], self.rank - 1, group=self.group)]
         if hi < Hg:
             bot = torch.empty_like(src[:, :, :g1 - hi]).contiguous()
+            sends.append(src[:, :, max(0, hi - lo - h):].clone(memory_format=torch.contiguous_format))
             ops += [dist.P2POp(dist.irecv, bot, self.rank + 1, group=self.group),
-                    dist.P2POp(dist.isend, src[:, :, max(0, hi - lo - h):].contiguous(), self.rank + 1,
-                               group=self.group)]
-        for req in dist.batch_isend_irecv(ops):
+                    dist.P2POp(dist.isend, sends[-1], self.rank + 1, group=self.group)]
+        return ("posted", t, g0, dist.batch_isend_irecv(ops), top, bot, staged, sends)
+
+    def _halo_finish(self, hd):
+        if hd[0] == "done":
+            return hd[1], hd[2]
+        _, t, g0, reqs, top, bot, staged, _sends = hd
+        dev = t.device
+        t0 = time.perf_counter()
+        for req in reqs:
             req.wait()
+        self.xchg_wait_s += time.perf_counter() - t0
+        self.xchg_count += 1
         seq = ([top.to(dev) if staged else top] if top is not None else []) + [t]
         seq += [bot.to(dev) if staged else bot] if bot is not None else []
         return torch.cat(seq, 2), g0
@@ -392,39 +432,75 @@ class RowShardedStereo:
                     x, lo, hi, Hg = self._run(blk, x, lo, hi, Hg, 4 if st == 2 else 2, st)
             assert (lo, hi) == (r0, r1), (lo, hi, r0, r1)
             H1, levels = Hg, [(lo, hi, Hg)]
-            xs = self._halo(x, lo, hi, Hg, 4)              # heads08 and conv2 read x
-            outs = [[self._run(hd, None, lo, hi, Hg, 3, 1, slab=(xs[0][:B], xs[1]))[0]
-                     for hd in cn.outputs08]]
-            # conv2 (ResidualBlock with InstanceNorm + 3x3 conv), both images
-            blk2, conv = m.conv2[0], m.conv2[1]
-            xx, gx = xs
-            ol, oh = lo - gx, hi - gx                      # own rows, slab-local
-            eps = blk2.norm1.eps
-            y = blk2.relu(_instance_norm_rows(blk2.conv1(xx), ol, oh, self.group, eps))
-            y = blk2.relu(_instance_norm_rows(blk2.conv2(y), ol, oh, self.group, eps))
-            fm = conv(xx + y)[:, :, ol:oh]
-            fmap1, fmap2 = fm[:B], fm[B:]
-            if n >= 2:
-                y = x[:B]
-                for i, blk in enumerate(cn.layer4):
+            xs = self._halo(x, lo, hi, Hg, 4)              # heads08, conv2 and layer4[0] read x
+
+            def level0_heads():
+                """heads08 and conv2 (ResidualBlock with InstanceNorm + 3x3
+                conv, both images) on the exchanged slab xs."""
+                o08 = [self._run(hd, None, lo, hi, Hg, 3, 1, slab=(xs[0][:B], xs[1]))[0]
+                       for hd in cn.outputs08]
+                blk2, conv = m.conv2[0], m.conv2[1]
+                xx, gx = xs
+                ol, oh = lo - gx, hi - gx                  # own rows, slab-local
+                eps = blk2.norm1.eps
+                y2 = blk2.relu(_instance_norm_rows(blk2.conv1(xx), ol, oh, self.group, eps))
+                y2 = blk2.relu(_instance_norm_rows(blk2.conv2(y2), ol, oh, self.group, eps))
+                fm = conv(xx + y2)[:, :, ol:oh]
+                return o08, fm[:B], fm[B:]
+
+            def chain(blocks, y, lo, hi, Hg, slab0, side):
+                """Run residual blocks in turn, each on its input's halo slab;
+                the first block's exchange of an output is posted before
+                ``side()`` runs (overlap) and waited for after it."""
+                done = side is None or not self.overlap
+                ran, res = False, None
+                for i, blk in enumerate(blocks):
                     st = blk.conv1.stride[0]
-                    y, lo, hi, Hg = self._run(blk, y, lo, hi, Hg, 4 if st == 2 else 2, st)
+                    need = 4 if st == 2 else 2
+                    if i == 0 and slab0 is not None:
+                        y, lo, hi, Hg = self._run(blk, None, lo, hi, Hg, need, st, slab=slab0)
+                        continue
+                    if not done:
+                        h = self._halo_start(y, lo, hi, Hg, need)
+                        res, ran, done = side(), True, True
+                        y, lo, hi, Hg = self._run(blk, None, lo, hi, Hg, need, st, slab=self._halo_finish(h))
+                    else:
+                        y, lo, hi, Hg = self._run(blk, y, lo, hi, Hg, need, st)
+                if side is not None and not ran:
+                    res = side()
+                return y, lo, hi, Hg, res
+
+            if n >= 2:
+                # layer4[0] (stride 2, 4 rows of halo) reads the same slab xs;
+                # the exchange of its output runs under heads08 + conv2
+                y, lo, hi, Hg, (o08, fmap1, fmap2) = chain(
+                    cn.layer4, None, lo, hi, Hg, (xs[0][:B], xs[1]), level0_heads)
+                outs = [o08]
                 levels.append((lo, hi, Hg))
-                ys = self._halo(y, lo, hi, Hg, 4)
-                outs.append([self._run(hd, None, lo, hi, Hg, 3, 1, slab=ys)[0] for hd in cn.outputs16])
+                ys = self._halo(y, lo, hi, Hg, 4)          # heads16 and layer5[0] read it
+                o16 = lambda: [self._run(hd, None, lo, hi, Hg, 3, 1, slab=ys)[0]  # noqa: E731
+                               for hd in cn.outputs16]
                 if n >= 3:
-                    for i, blk in enumerate(cn.layer5):
-                        st = blk.conv1.stride[0]
-                        y, lo, hi, Hg = self._run(blk, y, lo, hi, Hg, 4 if st == 2 else 2, st,
-                                                  slab=ys if i == 0 else None)
+                    y, lo3, hi3, Hg3, o16v = chain(cn.layer5, None, lo, hi, Hg, ys, o16)
+                    outs.append(o16v)
+                    lo, hi, Hg = lo3, hi3, Hg3
                     levels.append((lo, hi, Hg))
                     zs = self._halo(y, lo, hi, Hg, 2)
                     outs.append([self._run(hd, None, lo, hi, Hg, 1, 1, slab=zs)[0] for hd in cn.outputs32])
+                else:
+                    outs.append(o16())
+            else:
+                o08, fmap1, fmap2 = level0_heads()
+                outs = [o08]
             net = [torch.tanh(o[0]) for o in outs]
+            # context convs: every level's exchange posted first, then each
+            # level waited for and convolved in turn
+            rel = [torch.relu(o[1]) for o in outs]
+            hs = [self._halo_start(rel[l], *levels[l], 1) for l in range(len(outs))]
             inp = []
-            for l, (o, c) in enumerate(zip(outs, m.context_zqr_convs)):
+            for l, c in enumerate(m.context_zqr_convs[:len(outs)]):
                 ql, qh, qH = levels[l]
-                z = self._run(c, torch.relu(o[1]), ql, qh, qH, 1, 1)[0]
+                z = self._run(c, None, ql, qh, qH, 1, 1, slab=self._halo_finish(hs[l]))[0]
                 inp.append(list(z.split(dim=1, split_size=c.out_channels // 3)))
         return fmap1, fmap2, net, inp, levels, H1
 
@@ -494,6 +570,9 @@ class RowShardedStereo:
         xch = ((lambda t, l: self._exchange(t, l, own[l], ext[l], glob[l])) if self.per_stage
                else None)
         preds = []
+        if self.per_stage and self.overlap:
+            return self._forward_overlap(corr_fn, coords0, coords1, net, inp, interp, iters, own, ext,
+                                         glob, r0 - e0, r1 - e0)
         for _ in range(iters):
             corr = corr_fn(coords1)
             flow = coords1 - coords0
@@ -509,6 +588,66 @@ class RowShardedStereo:
             for l in range(1 if self.per_stage else nl):
                 net[l] = self._exchange(net[l], l, own[l], ext[l], glob[l])
             coords1 = self._exchange(coords1, 0, own[0], ext[0], glob[0])
+        return preds
+
+    def _forward_overlap(self, corr_fn, coords0, coords1, net, inp, interp, iters, own, ext, glob,
+                         o0, o1):
+        """The per-stage loop of ``forward`` with every exchange posted when
+        its rows are final and waited for right before its first reader
+        (model.py:374-383 order per tensor, so the values are those of the
+        blocking loop bit for bit):
+          gru32 -> post net[2]  | corr lookup + flow (after coords1 / net[0] of
+                                |   the previous iteration arrive)
+          wait net[2] -> gru16 -> post net[1] | motion encoder (flow, corr)
+          wait net[1] -> gru08 -> flow head -> coords1 update
+          post net[0] and coords1 | next iteration's gru32 (reads net[1],
+                                  |   net[2] only)."""
+        from .network import pool2x
+        m, a = self.model, self.model.args
+        blk = m.update_block
+        n = a.n_gru_layers
+        X = lambda t, l: self._exchange_start(t, l, own[l], ext[l], glob[l])  # noqa: E731
+        W = self._exchange_finish
+        preds, pend = [], None          # pend: (net[0], coords1) exchanges in flight
+
+        def settle():
+            nonlocal pend, coords1
+            if pend is not None:
+                net[0], coords1 = W(pend[0]), W(pend[1])
+                pend = None
+
+        for _ in range(iters):
+            with m._autocast():
+                if n == 3 and a.slow_fast_gru:       # gru32 only: needs net[1], net[2]
+                    net[2] = W(X(blk.gru32(net[2], *inp[2], pool2x(net[1])), 2))
+                if n >= 2 and a.slow_fast_gru:
+                    if n == 3:
+                        net[2] = W(X(blk.gru32(net[2], *inp[2], pool2x(net[1])), 2))
+                    settle()                         # gru16 pools net[0]
+                    extra = (interp(net[2], 2, 1),) if n > 2 else ()
+                    net[1] = W(X(blk.gru16(net[1], *inp[1], pool2x(net[0]), *extra), 1))
+                h2 = X(blk.gru32(net[2], *inp[2], pool2x(net[1])), 2) if n == 3 else None
+            settle()
+            corr = corr_fn(coords1)
+            flow = coords1 - coords0
+            with m._autocast():
+                if n >= 2:
+                    if h2 is not None:
+                        net[2] = W(h2)
+                    extra = (interp(net[2], 2, 1),) if n > 2 else ()
+                    h1 = X(blk.gru16(net[1], *inp[1], pool2x(net[0]), *extra), 1)
+                    motion = blk.encoder(flow, corr)
+                    net[1] = W(h1)
+                else:
+                    motion = blk.encoder(flow, corr)
+                extra = (interp(net[1], 1, 0),) if n > 1 else ()
+                net[0] = blk.gru08(net[0], *inp[0], motion, *extra)
+                delta = blk.flow_head(net[0])
+            delta[:, 1] = 0.0
+            coords1 = coords1 + delta.float()
+            preds.append((coords1 - coords0)[:, :, o0:o1])
+            pend = (X(net[0], 0), X(coords1, 0))
+        settle()
         return preds
 
     @staticmethod

@@ -29,7 +29,7 @@ def row_case():
     return f1, f2, torch.cat([x, torch.zeros(2, 1, 7, 24)], 1)
 
 
-def model():
+def model(slow_fast=False):
     import torch
     import pkgload
     pkgload.load()
@@ -38,7 +38,10 @@ def model():
     from raft_stereo_amd.network import RAFTStereo, StereoArgs
     torch.manual_seed(0)
     case = manifest()["cases"]["e2e_default"]
-    return RAFTStereo(StereoArgs(**case["args"]), corr_block=torch_ref.TorchCorrBlock1D).eval()
+    args = dict(case["args"])
+    if slow_fast:
+        args["slow_fast_gru"] = True
+    return RAFTStereo(StereoArgs(**args), corr_block=torch_ref.TorchCorrBlock1D).eval()
 
 
 def run(rank, world, port, q):
@@ -71,7 +74,7 @@ def run(rank, world, port, q):
 
 
 def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders=True,
-             per_stage=False):
+             per_stage=False, overlap=True, slow_fast=False):
     """Row-sharded network forward vs the unsharded one (oracle corr block)."""
     import torch
     import torch.distributed as dist
@@ -86,9 +89,9 @@ def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders
         g = torch.Generator().manual_seed(3)
         img1 = torch.rand(1, 3, H, W, generator=g) * 255
         img2 = torch.roll(img1, -4, dims=-1)
-        net = model()
+        net = model(slow_fast=slow_fast)
         rs = RowShardedStereo(net, rank, world, halo=halo, shard_encoders=shard_encoders,
-                              per_stage=per_stage)
+                              per_stage=per_stage, overlap=overlap)
         with torch.no_grad():
             preds = rs.forward(img1, img2, iters=iters)
             full = [rs.gather_rows(p) for p in preds]

@@ -170,6 +170,41 @@ def test_autograd_deferred_equals_per_call(L):
         assert norm_err(x, y) <= 1e-5 and rel_l2(x, y) <= 1e-6
 
 
+def test_autograd_deferred_bounded_retention():
+    """the deferred state holds at most max_pending_calls recorded
+    calls (here 3 of 7: partial passes of 3, 3, then 1 at the build node, the
+    first overwriting, the rest adding) and stores every grad_out as contiguous
+    fp32 when it is recorded (channels_last gradients here); the fmap
+    gradients equal the one-pass deferred sum within the fp32 contract."""
+    B, D, H, W1, W2, L, r, calls = 2, 32, 3, 50, 96, 4, 4, 7
+    g = torch.Generator().manual_seed(71)
+    f1 = torch.randn(B, D, H, W1, generator=g)
+    f2 = torch.randn(B, D, H, W2, generator=g)
+    cs, gs = make_calls(B, H, W1, W2, L, r, calls, seed=72)
+    grads, seen = {}, []
+    for cap in (32, 3):
+        a = f1.to(DEV).requires_grad_(True)
+        b = f2.to(DEV).requires_grad_(True)
+        blk = CorrBlock1D(a, b, num_levels=L, radius=r)
+        st = blk._state
+        st.max_pending_calls = cap
+        flush = st._flush
+
+        def spy(flush=flush, st=st):
+            seen.append((cap, len(st.pending)))
+            assert all(go.dtype == torch.float32 and go.is_contiguous() for _, go in st.pending)
+            flush()
+        st._flush = spy
+        outs = [blk(c.to(DEV)) for c in cs]
+        gos = [x.to(DEV).contiguous(memory_format=torch.channels_last) for x in gs]
+        torch.autograd.backward(outs, gos)
+        assert not st.pending and st.pending_bytes == 0
+        grads[cap] = (a.grad.cpu().numpy(), b.grad.cpu().numpy())
+    assert [n for c, n in seen if c == 3] == [3, 3, 1] and [n for c, n in seen if c == 32] == [7]
+    for x, y in zip(grads[3], grads[32]):
+        assert norm_err(x, y) <= 1e-5 and rel_l2(x, y) <= 1e-6
+
+
 @pytest.mark.parametrize("spread", ["bench", "whole_row"])
 def test_compact_equals_whole_row_kernel(spread):
     """The compact-row kernel (RAFTCORR_BWDC_VARIANT=3; the launcher's choice

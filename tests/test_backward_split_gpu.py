@@ -95,3 +95,25 @@ def test_split_volume_backward_through_autograd_exact_flag():
     for x_, y_ in zip(grads[False], grads[True]):
         assert norm_err(x_, y_) <= 1e-5 and rel_l2(x_, y_) <= 1e-6
         assert not np.array_equal(x_, y_)
+
+
+def test_split_volume_backward_dev_variant2_equals_product():
+    """Dev A/B variant RAFTCORR_VBWD_VARIANT=2 (G^T staged by the non-k-major
+    mapping, buffer loads) computes the product's dF1 / dF2 bit for bit
+    (its buffer-load staging used the k-major mapping)."""
+    import os
+    from raft_stereo_amd import _lib
+    B, D, H, W1, W2 = 2, 256, 2, 240, 240
+    g = torch.Generator().manual_seed(21)
+    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
+    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
+    bufs, _ = level_grads(B * H * W1, [W2 >> i for i in range(4)], "pair4", g)
+    ref = rcorr.build_backward(f1, f2, bufs)
+    with _lib.dev_library():
+        try:
+            os.environ["RAFTCORR_VBWD_VARIANT"] = "2"
+            got = rcorr.build_backward(f1, f2, bufs)
+        finally:
+            os.environ["RAFTCORR_VBWD_VARIANT"] = "0"
+    for x_, y_ in zip(got, ref):
+        assert torch.equal(x_, y_)

@@ -102,6 +102,24 @@ def test_gloo_row_sharded_network(world, halo, H, W, shard_enc, per_stage):
         assert (got - ref).abs().mean() < 1e-6
 
 
+@pytest.mark.parametrize("world,slow_fast", [(3, False), (2, True)])
+def test_gloo_overlapped_exchanges_equal_blocking(world, slow_fast):
+    """with ``overlap`` (the default) every halo exchange
+    -- the encoders' per-module halos and the GRU's per-stage ones -- is
+    posted when its rows are final and waited for right before its first
+    reader, with independent work in between (model.py:374-383 per tensor);
+    the per-iteration flows equal the blocking order's bit for bit, with and
+    without the slow-fast GRU schedule."""
+    H, W, iters = 800, 64, 3
+    got = {}
+    for overlap in (True, False):
+        res = _spawn(dist_worker.run_rows, world, 12, H, W, iters, True, True, overlap, slow_fast)
+        got[overlap] = res[0][0]
+        for r in range(world):
+            assert torch.equal(res[r][0], got[overlap])
+    assert torch.equal(got[True], got[False])
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_row_sharded_encoders_match_full(world):
     """each rank's encoder band (its GRU slab + 48

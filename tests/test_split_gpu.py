@@ -111,3 +111,43 @@ def test_split_special_values():
         r, s = ref[:, :, w1], sp[:, :, w1]
         if np.abs(r).max() > 0:
             assert norm_err(s, r) <= 1e-5, w1
+
+
+def test_split_nonfinite_fmaps_pinned():
+    """Non-finite fmap entries (model.py:324-326 on +-inf / NaN inputs).
+
+    The exact fp32 kernel (exact_f32=True / RC_BUILD_EXACT_F32) reproduces
+    the reference's pattern: +-inf where an inf meets finite values, NaN where
+    a NaN is involved or infinities of both signs meet.  The split-bf16 default
+    is PINNED to a documented difference: an
+    inf operand splits into pieces (inf, NaN, NaN), so every entry the
+    reference makes +-inf comes out NaN.  Everything the reference keeps
+    finite stays finite and within the fp32 bound, and the non-finite SET is
+    the reference's in both kernels.  (A guard that zeroes the tail pieces of a
+    non-finite head cannot fix it: the head then meets zero tail pieces of the
+    other operand in the h*m' and h*l' products, and inf * 0 is NaN on the
+    MFMA as anywhere.)"""
+    B, D, H, W = 1, 64, 3, 96
+    g = torch.Generator().manual_seed(11)
+    f1 = torch.randn(B, D, H, W, generator=g)
+    f2 = torch.randn(B, D, H, W, generator=g)
+    f1[0, 5, 0, 7] = float("inf")
+    f1[0, 9, 1, 20] = float("-inf")
+    f1[0, 2, 2, 33] = float("nan")
+    f2[0, 17, 0, 50] = float("inf")
+    f2[0, 17, 1, 60] = float("-inf")
+    f1[0, 30, 1, 20] = float("inf")          # row w1=20 of h=1 meets +inf and -inf: NaN
+    ref = coracle.corr_volume(f1.numpy(), f2.numpy())
+    with torch.no_grad():
+        sp = CorrBlock1D.corr(f1.to(DEV), f2.to(DEV)).cpu().numpy()
+        ex = CorrBlock1D.corr(f1.to(DEV), f2.to(DEV), exact_f32=True).cpu().numpy()
+    fin = np.isfinite(ref)
+    assert (~fin).sum() > 0 and np.isnan(ref).sum() > 0 and np.isinf(ref).sum() > 0
+    for got in (ex, sp):
+        assert np.array_equal(np.isfinite(got), fin)
+        assert norm_err(got[fin], ref[fin]) <= 1e-4
+    # exact kernel: the reference's infinities (sign included) and NaNs
+    assert np.array_equal(np.isnan(ex), np.isnan(ref))
+    assert np.array_equal(ex[np.isinf(ref)], ref[np.isinf(ref)])
+    # split default: NaN wherever the reference is non-finite (the pinned difference)
+    assert np.isnan(sp[~fin]).all()

@@ -101,6 +101,14 @@ if has pmcl; then   # lookup variants: L1->L2 request count / latency, L2 hits, 
     { python tools/pmc_raw.py "$OUT/pmc_l1" --width 90; python tools/pmc_raw.py "$OUT/pmc_l2" --width 90;
       python tools/pmc_raw.py "$OUT/pmc_l3" --width 90; } > "$OUT/pmc_l.txt" 2>&1; grep lookup "$OUT/pmc_l.txt"
 fi
+if has proj; then   # per-rank shapes at N = 1/2/4/8 on one GPU (projection inputs)
+    for N in 1 2 4 8; do
+        step proj_kitti_$N 300 python bench.py --config kitti --per-rank-of $N --no-cpu-baseline --steps 10 --warmup 3
+        step proj_middlebury_$N 300 python bench.py --config middlebury --per-rank-of $N --no-cpu-baseline --steps 5 --warmup 2
+    done
+fi
+has shard8 && step shard_probe_h8 900 python tools/shard_probe.py --halo 8
+has train && step train_probe 300 python tools/train_probe.py
 has lprobe2 && step lookup_probe2 600 python tools/lookup_probe.py --only-dev --dev-variants ${LPROBE_VARIANTS:-215} --dev-fields ${LPROBE_FIELDS:-bench,smooth,net} --reps ${LPROBE_REPS:-7}
 if has calib; then   # FETCH_SIZE / WRITE_SIZE per byte for scattered 64-256 B rows
     step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o f \

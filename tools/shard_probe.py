@@ -24,6 +24,14 @@ then T(N) = E + C(n_N) + iters * U(n_N) (halo exchange not included: a few
 MB per neighbour per iteration over xGMI, tens of us) and the speedup
 T(1) / T(N).  The replicated encoder bounds it: T(N) >= E; with sharded
 encoders Ts(N) = Es(N) + C(n_N) + iters * U(n_N).
+
+    python tools/shard_probe.py --xchg [--world 3]
+
+Exposed exchange time instead: ``world`` CPU processes
+over gloo run RowShardedStereo.forward on a small image with the exchanges
+overlapped (the default) and blocking, and report per rank the forward time,
+the host time blocked in exchange waits (``xchg_wait_s``) and the number of
+waits.  A CPU/gloo rehearsal of the schedule, not an xGMI measurement.
 """
 import argparse
 import json
@@ -55,6 +63,58 @@ def timed(fn, reps=3):
     return ts[len(ts) // 2]
 
 
+def _xchg_rank(rank, world, port, q, H, W, iters, threads):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(threads)
+    try:
+        from oracle import torch_ref   # CPU processes: the ATen corr block
+        torch.manual_seed(0)
+        model = RAFTStereo(StereoArgs(), corr_block=torch_ref.TorchCorrBlock1D).eval()
+        g = torch.Generator().manual_seed(1234)
+        img1 = torch.rand(1, 3, H, W, generator=g) * 255
+        img2 = torch.roll(img1, -8, dims=-1)
+        out = {}
+        with torch.no_grad():
+            for overlap in (True, False, True, False):
+                rs = RowShardedStereo(model, rank, world, overlap=overlap)
+                dist.barrier()
+                t0 = time.perf_counter()
+                rs.forward(img1, img2, iters=iters)
+                t = time.perf_counter() - t0
+                out["overlap" if overlap else "blocking"] = {
+                    "forward_s": round(t, 3), "xchg_wait_s": round(rs.xchg_wait_s, 3),
+                    "waits": rs.xchg_count, "exposed_frac": round(rs.xchg_wait_s / t, 3)}
+        q.put((rank, out))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def xchg_main(world, H, W, iters):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    threads = max(1, (os.cpu_count() or 2) // world)
+    ps = [ctx.Process(target=_xchg_rank, args=(r, world, port, q, H, W, iters, threads))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=1800) for _ in ps)
+    for p in ps:
+        p.join()
+    print(json.dumps({"rehearsal": "CPU processes over gloo (not xGMI)", "world": world,
+                      "image": [H, W], "iters": iters, "threads_per_rank": threads,
+                      "per_rank": {r: res[r] for r in sorted(res)}}, indent=1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=32)
@@ -62,7 +122,12 @@ def main():
                     help="1/4-res halo rows (12: per-stage exchange, the default; 32: once per iteration)")
     ap.add_argument("--H", type=int, default=1984)
     ap.add_argument("--W", type=int, default=2880)
+    ap.add_argument("--xchg", action="store_true", help="exposed-exchange rehearsal (gloo, CPU)")
+    ap.add_argument("--world", type=int, default=3)
     a = ap.parse_args()
+    if a.xchg:
+        return xchg_main(a.world, 768 if a.H == 1984 else a.H, 256 if a.W == 2880 else a.W,
+                         8 if a.iters == 32 else a.iters)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = RAFTStereo(StereoArgs()).eval().to(dev)

@@ -63,6 +63,22 @@ def main():
         gpu.sort()
         res[name] = {"wall_ms": round(wall[len(wall) // 2], 3), "gpu_ms": round(gpu[len(gpu) // 2], 3)}
         print(name, res[name], flush=True)
+    # Peak device memory of one step: the loss multiplies every
+    # lookup output by a weight, so each call's output gradient is a fresh
+    # tensor (as in the network) that the deferred state keeps until the build
+    # node, where the per-call backward frees it after its own call.
+    for name, deferred in (("mem_deferred", None), ("mem_per_call", False)):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        blk = CorrBlock1D(fa, fb, num_levels=L, radius=r, grad_deferred=deferred)
+        loss = sum((blk(coords[it]) * gl[it]).sum() for it in range(iters))
+        loss.backward()
+        torch.cuda.synchronize()
+        res[name] = {"peak_above_inputs_MB": round((torch.cuda.max_memory_allocated() - base) / 1e6, 1)}
+        print(name, res[name], flush=True)
+        del blk, loss
     print(json.dumps(res))
 
 
