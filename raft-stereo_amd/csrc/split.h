@@ -23,16 +23,29 @@ struct SplitFrag {
     bf16x8 h, m, l;
 };
 
+// a - b as ONE scalar v_sub_f32: opaque to the SLP vectorizer, which would
+// pair the residuals of two elements into v_pk_add_f32 -- beside MFMAs a
+// packed f32 op costs ~4x the issue slots of two scalar ones
+// (MI355X_MICROARCH.md, constants table: "an anti-lever beside MFMAs")
+__device__ __forceinline__ float sp_sub(float a, float b) {
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // 8 consecutive d of one w -> head, middle and low bf16 pieces (each exact
 // residual of the previous: x = h + m + l for finite |x| < 3.39e38).
+// SCALAR: residuals by sp_sub (v_sub_f32) instead of compiler-packed ops.
+template <bool SCALAR = false>
 __device__ __forceinline__ SplitFrag sp_split(const float (&x)[8]) {
     u32x4s h, m, l;
+    auto sub = [](float a, float b) { return SCALAR ? sp_sub(a, b) : a - b; };
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t hp = sp_pack(x[2 * k], x[2 * k + 1]);
-        const float r0 = x[2 * k] - sp_lo(hp), r1 = x[2 * k + 1] - sp_hi(hp);      // exact
+        const float r0 = sub(x[2 * k], sp_lo(hp)), r1 = sub(x[2 * k + 1], sp_hi(hp));   // exact
         const uint32_t mp = sp_pack(r0, r1);
-        const float s0 = r0 - sp_lo(mp), s1 = r1 - sp_hi(mp);                      // exact
+        const float s0 = sub(r0, sp_lo(mp)), s1 = sub(r1, sp_hi(mp));                  // exact
         h[k] = hp;
         m[k] = mp;
         l[k] = sp_pack(s0, s1);
@@ -49,6 +62,19 @@ __device__ __forceinline__ void sp_mma6(f32x4 &c, const SplitFrag &x, const Spli
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.m, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.m, y.h, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.h, c, 0, 0, 0);
+}
+
+// The same six products on v_mfma_f32_32x32x16_bf16 (32 cycles per SIMD, of
+// which it holds the vector issue for 8: three times the room for the split's
+// VALU per MFMA cycle of the 16x16x32 form, whose 16 cycles hold it for 8).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ void sp_mma6_32(f32x16 &c, const SplitFrag &x, const SplitFrag &y) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.m, y.m, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.h, y.l, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.l, y.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.h, y.m, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.m, y.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.h, y.h, c, 0, 0, 0);
 }
 
 }  // namespace rc

@@ -67,7 +67,7 @@ __device__ __forceinline__ SplitFrag sp_read(const char *base) {
         const bf16x8 hb = __builtin_bit_cast(bf16x8, h);
         return SplitFrag{hb, hb, hb};
     }
-    return sp_split(x);
+    return sp_split<(MODE & kModeScalarSub) != 0>(x);
 }
 
 struct SpCtx {
@@ -112,6 +112,17 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
     for (int x0 = 0; x0 < (FA > 0 ? FA : 1); ++x0)
 #pragma unroll
         for (int y0 = 0; y0 < 4; ++y0) acc[x0][y0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // kMode32: 32-wide fragments (ceil of the 16-wide counts)
+    constexpr int FA2 = (FA + 1) / 2 > 0 ? (FA + 1) / 2 : 1, FB2 = (FB + 1) / 2;
+    f32x16 acc32[(MODE & kMode32) ? FA2 : 1][(MODE & kMode32) ? FB2 : 1];
+    if constexpr ((MODE & kMode32) != 0) {
+#pragma unroll
+        for (int x0 = 0; x0 < FA2; ++x0)
+#pragma unroll
+            for (int y0 = 0; y0 < FB2; ++y0)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc32[x0][y0][r] = 0.f;
+    }
     const int nks = (c.nst + 1) >> 1;                     // K steps (the launcher pads nst to even)
     // stages of K steps 0 and 1 in flight
 #pragma unroll
@@ -130,7 +141,26 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
             sp_issue<MODE>(c, smem, 2 * ks + 2);
             sp_issue<MODE>(c, smem, 2 * ks + 3);
         }
-        if constexpr (FA > 0 && !(MODE & kModeNoMath)) {
+        if constexpr (FA > 0 && !(MODE & kModeNoMath) && (MODE & kMode32)) {
+            // 32x32x16 form: each 16-d stage is one MFMA k-step; lane
+            // (r = l & 31, h = l >> 5) reads rows 8h..8h+7 at column r of
+            // its 32-wide fragments (dev A/B, kMode32)
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) {
+                const char *st = smem + ((2 * ks + sub) % kSpSL) * kSpSlot + (lane >> 5) * 4 * kSpBlk;
+                const char *pb = st + 4 * (c.o1 + (lane & 31));
+                const char *pa = st + kSpOp + 4 * (c.o2 + (lane & 31));
+                SplitFrag fb2[FB2];
+#pragma unroll
+                for (int n = 0; n < FB2; ++n) fb2[n] = sp_read<MODE>(pb + 128 * n);
+#pragma unroll
+                for (int m = 0; m < FA2; ++m) {
+                    const SplitFrag fa = sp_read<MODE>(pa + 128 * m);
+#pragma unroll
+                    for (int n = 0; n < FB2; ++n) sp_mma6_32(acc32[m][n], fa, fb2[n]);
+                }
+            }
+        } else if constexpr (FA > 0 && !(MODE & kModeNoMath)) {
             const char *st = smem + ((2 * ks + (g >> 1)) % kSpSL) * kSpSlot + lrow;
             const char *pb = st + 4 * (c.o1 + i);                        // F1 (B): this wave's w1
             const char *pa = st + kSpOp + 4 * (c.o2 + i);                // F2 (A): this wave's w2
@@ -188,6 +218,29 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
                 }
             }
         }
+    }
+    if constexpr (FA > 0 && (MODE & kMode32) != 0) {
+        // 32x32 layout (lane l: w1 = 32n + (l & 31), w2 = 32m + (R & 3) +
+        // 8(R >> 2) + 4(l >> 5)) -> the 16x16 layout epilogue_swapped takes
+        // (lane 16g + i: w1 = 16nb + i, w2 = 16ma + 4g + r): lane 16g + i reads
+        // lane 32(g & 1) + 16(nb & 1) + i, register 4(2(ma & 1) + (g >> 1)) + r
+#pragma unroll
+        for (int ma = 0; ma < FA; ++ma)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                if (nb >= 2 * FB2) {
+                    acc[ma][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    continue;
+                }
+                const int src = 32 * (g & 1) + 16 * (nb & 1) + i;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v0 = acc32[ma >> 1][nb >> 1][8 * (ma & 1) + r];
+                    const float v1 = acc32[ma >> 1][nb >> 1][8 * (ma & 1) + 4 + r];
+                    const float a0 = __shfl(v0, src, 64), a1 = __shfl(v1, src, 64);
+                    acc[ma][nb][r] = (g >> 1) ? a1 : a0;
+                }
+            }
     }
     // the ring becomes the waves' epilogue staging images
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -575,6 +628,9 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         case 1027: hipLaunchKernelGGL((rc::build_split_kernel<1027, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 515: hipLaunchKernelGGL((rc::build_split_kernel<515, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 256: hipLaunchKernelGGL((rc::build_split_kernel<256, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 8192: hipLaunchKernelGGL((rc::build_split_kernel<8192, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 16384: hipLaunchKernelGGL((rc::build_split_kernel<16384, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 24576: hipLaunchKernelGGL((rc::build_split_kernel<24576, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         default: break;
     }
 #endif

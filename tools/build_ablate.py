@@ -74,6 +74,8 @@ def main():
                 got = run(v)().corr_pyramid[:1]
                 res.setdefault("bit_identical", {})[str(v)] = all(
                     bool(torch.equal(x, y)) for x, y in zip(got, ref))
+                res.setdefault("norm_err_vs_0", {})[str(v)] = max(
+                    float((x - y).abs().max() / y.abs().max()) for x, y in zip(got, ref))
         for _ in range(a.rounds):
             for v in variants:
                 fn = run(v)
@@ -81,9 +83,11 @@ def main():
         os.environ["RAFTCORR_SPLIT_MODE"] = "0"
         os.environ["RAFTCORR_SPLIT_KERNEL"] = "0"
     ident = res.pop("bit_identical", {})
+    nerr = res.pop("norm_err_vs_0", {})
     out = {k: {"median_us": statistics.median(x), "min_us": min(x)} for k, x in res.items()}
     for k, v in ident.items():
         out[k]["bit_identical"] = v
+        out[k]["norm_err_vs_mode0"] = nerr[k]
     flops = bench.volume_flops(B, D, H, W1, W2)
     for k, v in out.items():
         v["fp32_equiv_tflops"] = flops / (v["median_us"] * 1e-6) / 1e12
