@@ -892,6 +892,73 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+#ifdef RAFTCORR_DEV
+// Disparity-major ("sheared") pair lookup (dev only): the
+// pair kernel's arithmetic (levels 0 and 2 stored, 1 and 3 their pairwise
+// means, finish_pair) over levels stored as S_i[b,h][k][w1] with
+// k = (w1 >> i) - j + W_i - 1 (lookup_sheared.hip's layout), so the lanes of
+// a wave whose pixels look at the same disparity read one contiguous run of
+// a row per span element -- coalesced along w1 -- instead of a 16-B piece of
+// 64 different pixel rows.  A span is 2(2r+4) dword loads per lane (exact-
+// span predicated).  No memory fallback (finish_pair NOFALLBACK): the probe
+// feeds no subnormal coordinates.
+template <int R>
+__global__ __launch_bounds__(256) void lookup_sheared_pair_kernel(LookupArgs a, const float *s0, const float *s2,
+                                                                  long long K0, long long K2, long long ldw) {
+    constexpr int NS = PairSpan<R>::NS;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const long long pblk = (long long)blk * 256;
+    const long long p = pblk + threadIdx.x;
+    const bool active = p < a.P;
+    const long long pp = active ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    const float x = pixel_x(a, bimg, rem, active);
+    const int H = a.HW / a.W1;
+    const int h = (int)(rem / a.W1), w1 = (int)(rem - (long long)h * a.W1);
+    const long long bh = bimg * H + h, bh0 = pblk / a.W1;          // bh0: block-uniform
+    float *outp = a.out + bimg * (long long)(4 * (2 * R + 1)) * a.HW + rem;
+    auto sink = [&](int ch, float v) {
+        if (active) outp[(long long)ch * a.HW] = v;
+    };
+    PairSpan<R> sp[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int lo = 2 * k;
+        PairSpan<R> &ps = sp[k];
+        const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+        const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+        ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));
+        ps.m = ps.inwin ? floorf(xhi) : 0.0f;
+        ps.n = ps.inwin ? floorf(xlo) : 0.0f;
+        const int dd = (int)ps.n - 2 * (int)ps.m;
+        ps.valid = ps.inwin && (dd == 0 || dd == 1);
+        int lo_e = 0x7FFFFFFF, hi_e = -1;
+        if (ps.inwin) {
+            int f, l;
+            tap_span<R>(xlo, Wlo, f, l);
+            if (f <= l) { lo_e = f; hi_e = l; }
+            tap_span<R>(xhi, Whi, f, l);
+            if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
+        }
+        ps.sh = 0;
+        const int sa = 2 * ((int)ps.m - R - 1);
+        const long long K = k ? K2 : K0;
+        const float *lv = k ? s2 : s0;
+        const auto rs = make_rsrc(lv + bh0 * K * ldw, clamp_bytes((a.P / a.W1 - bh0) * K * ldw * 4));
+        const long long rowk = (bh - bh0) * K + (w1 >> lo) + Wlo - 1;    // row of element 0
+#pragma unroll
+        for (int c = 0; c < PairSpan<R>::NC * 4; ++c) {
+            const int j = sa + c;
+            const bool ok = c < NS && j >= lo_e && j <= hi_e;
+            const uint32_t off = ok ? (uint32_t)(((rowk - j) * ldw + w1) * 4) : 0xFFFFFF00u;
+            ps.q[c >> 2][c & 3] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) finish_pair<R, true>(sp[k], a, 2 * k, x, pp, sink);
+}
+#endif
+
 // Persistent pair lookup (dev variants 215-219 while measured).  The one-round
 // grid of lookup_pair_kernel puts every wave in the same phase: all spans are
 // requested at launch and each wave's output stores follow its own loads.
@@ -1458,6 +1525,30 @@ hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, h
         default: return hipErrorInvalidValue;
     }
 }
+
+#ifdef RAFTCORR_DEV
+// Dev-only entry: the sheared pair lookup (fp32, 4 levels, r = 4) over levels
+// 0 and 2 stored as S_i[b,h][k][w1] (K0 / K2 rows of ldw floats per image row).
+extern "C" int rc_dev_lookup_sheared_pair(const void *lvl0, const void *lvl2, long K0, long K2, long ldw,
+                                          const int *widths, const float *coords_x, long cbs, int B, int H,
+                                          int W1, float *out, void *stream) {
+    rc::LookupArgs a{};
+    for (int i = 0; i < 4; ++i) a.W[i] = widths[i];
+    a.coords = coords_x;
+    a.cbs = cbs;
+    a.out = out;
+    a.P = (long long)B * H * W1;
+    a.HW = H * W1;
+    a.W1 = W1;
+    a.levels = 4;
+    if (a.P <= 0) return 0;
+    const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    hipLaunchKernelGGL((rc::lookup_sheared_pair_kernel<4>), dim3(nblk), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), a, static_cast<const float *>(lvl0),
+                       static_cast<const float *>(lvl2), (long long)K0, (long long)K2, (long long)ldw);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+#endif
 
 hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;

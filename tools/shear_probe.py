@@ -1,14 +1,20 @@
-"""A/B of the row-major vs disparity-major ("sheared") pyramid for the lookup.
+"""A/B of the row-major pair lookup (the product) vs the disparity-major
+("sheared") pair lookup.
 
-    python tools/shear_probe.py [--config sceneflow] [--reps 20]
+    python tools/shear_probe.py [--config sceneflow] [--reps 7]
 
-Builds the product (row-major) pyramid with CorrBlock1D, re-lays it out as
-S_i[b,h][k][w1] (k = (w1>>i) - j + W_i - 1, see csrc/lookup_sheared.hip) with
-torch indexing, and times both lookups on three disparity fields:
+Builds the product pyramid (levels 0 and 2 stored) with CorrBlock1D, re-lays
+levels 0 and 2 out as S_i[b,h][k][w1] (k = (w1>>i) - j + W_i - 1) with torch
+indexing, and times both lookups -- the same pair arithmetic and Markstein
+division, bit-identical outputs (checked) -- on five disparity fields, 32
+launches each, interleaved:
   random: coords_grid - U[0,64) per pixel (the bench's field);
   smooth: coords_grid - a smooth field in [0,64) (bilinear from a 9x16 grid);
-  zero:   coords_grid (flow_init = 0, the first iteration).
-Checks that both layouts give bit-identical results.
+  slant:  planar surfaces, |slope| <= 0.25 px/px;
+  zero:   coords_grid (flow_init = 0, the first iteration);
+  net:    coords1 of network.RAFTStereo's iterations at 540x960 (tools/lookup_probe.py).
+(Round 1's sheared prototype -- all four levels stored, one window per level
+-- is in profiles/r01/shear_probe.log.)
 """
 import argparse
 import ctypes
@@ -22,6 +28,7 @@ import torch.nn.functional as F
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 import bench  # noqa: E402
 from raft_stereo_amd import CorrBlock1D, coords_grid  # noqa: E402
 from raft_stereo_amd import _lib  # noqa: E402
@@ -54,80 +61,81 @@ def make_coords(kind, B, H, W1, n, seed):
     return out
 
 
-def shear(pyr, B, H, W1, L, ldw):
-    levels, K = [], []
-    for i in range(L):
+def shear_pair(pyr, B, H, W1):
+    """Levels 0 and 2 of the product pyramid as S_i[b,h][k][w1] (the sheared
+    pair kernel's layout, csrc/lookup.hip lookup_sheared_pair_kernel)."""
+    out, K = [], []
+    for i in (0, 2):
         Wi = pyr[i].shape[-1]
         C = pyr[i].reshape(B * H, W1, Wi)
         Ki = Wi + ((W1 - 1) >> i)
-        S = torch.zeros(B * H, Ki, ldw, device=C.device)
+        S = torch.zeros(B * H, Ki, W1, device=C.device)
         w1 = torch.arange(W1, device=C.device)
         j = torch.arange(Wi, device=C.device)
         kk = (w1 >> i)[:, None] - j[None, :] + Wi - 1
         S[:, kk, w1[:, None].expand(W1, Wi)] = C
-        levels.append(S)
+        out.append(S.contiguous())
         K.append(Ki)
-    return levels, K
+    return out, K
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="sceneflow")
-    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=7)
     a = ap.parse_args()
     B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
-    lib = _lib.dev_library().__enter__()   # the prototype lives in the dev build only
-    fn = lib.rc_dev_lookup_sheared
+    lib = _lib.dev_library().__enter__()   # the sheared kernel lives in the dev build only
+    fn = lib.rc_dev_lookup_sheared_pair
     fn.restype = ctypes.c_int
     vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
-    fn.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(ci), ctypes.POINTER(cl), cl, ci, ci, vp, cl,
-                   ci, ci, ci, vp, vp]
-    ldw = (W1 + 63) // 64 * 64
+    fn.argtypes = [vp, vp, cl, cl, cl, ctypes.POINTER(ci), vp, cl, ci, ci, ci, vp, vp]
     res = {}
     with torch.no_grad():
         g = torch.Generator().manual_seed(0)
         f1 = torch.randn(B, D, H, W1, generator=g).cuda()
         f2 = torch.randn(B, D, H, W2, generator=g).cuda()
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r)
-        S, K = shear(blk.corr_pyramid, B, H, W1, L, ldw)
+        assert blk.levels_stored == [0, 2]
+        S, K = shear_pair(blk.corr_pyramid, B, H, W1)
+        widths = _lib.int_array([W2 >> i for i in range(4)])
         out = torch.empty(B, L * (2 * r + 1), H, W1, device="cuda")
         stream = torch.cuda.current_stream().cuda_stream
 
         def sheared(c):
-            rc = fn(_lib.ptr_array([t.data_ptr() for t in S]),
-                    _lib.int_array([t.shape[-1] for t in blk.corr_pyramid[:L]]),
-                    _lib.long_array(K), ldw, L, r, c.data_ptr(), 2 * H * W1, B, H, W1,
-                    out.data_ptr(), stream)
+            rc = fn(S[0].data_ptr(), S[1].data_ptr(), K[0], K[1], W1, widths, c.data_ptr(),
+                    2 * H * W1, B, H, W1, out.data_ptr(), stream)
             assert rc == 0, rc
             return out
 
-        variants = [("rows", blk, "0"), ("rows_unrolled", blk, "4"),
-                    ("sheared", sheared, "0"), ("sheared_unrolled", sheared, "3")]
-        for kind in ("random", "smooth", "slant", "zero"):
-            cs = make_coords(kind, B, H, W1, 4, seed=3)
-            for c in cs:
-                os.environ["RAFTCORR_LOOKUP_VARIANT"] = "0"
+        variants = [("product_pair", blk), ("sheared_pair", sheared)]
+        for kind in ("random", "smooth", "slant", "zero", "net"):
+            if kind == "net":
+                from lookup_probe import net_coords
+                cs = net_coords(B, H, W1, iters, torch.device("cuda", 0))
+            else:
+                cs = make_coords(kind, B, H, W1, iters, seed=3)
+            for c in cs[:4]:
                 ref = blk(c).clone()
-                for name, f, v in variants:
-                    os.environ["RAFTCORR_LOOKUP_VARIANT"] = v
-                    got = f(c)
-                    assert torch.equal(ref, got), (kind, name, (ref - got).abs().max().item())
-            for name, f, v in variants:
-                os.environ["RAFTCORR_LOOKUP_VARIANT"] = v
-                for _ in range(3):
-                    f(cs[0])
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
-                ev[0].record()
-                for k in range(a.reps):
-                    f(cs[k % len(cs)])
-                    ev[k + 1].record()
-                torch.cuda.synchronize()
-                ts = [ev[k].elapsed_time(ev[k + 1]) * 1e3 for k in range(a.reps)]
-                res[f"{kind}_{name}"] = {"median_us": statistics.median(ts), "min_us": min(ts)}
+                got = sheared(c)
+                assert torch.equal(ref, got), (kind, (ref - got).abs().max().item())
+            per = {n: [] for n, _ in variants}
+            for _ in range(a.reps):                  # interleaved: one 32-launch sequence each
+                for name, f in variants:
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(cs) + 1)]
+                    torch.cuda._sleep(3_000_000)
+                    ev[0].record()
+                    for k, c in enumerate(cs):
+                        f(c)
+                        ev[k + 1].record()
+                    torch.cuda.synchronize()
+                    per[name] += [ev[k].elapsed_time(ev[k + 1]) * 1e3 for k in range(len(cs))]
+            for name, _ in variants:
+                res[f"{kind}_{name}"] = {"median_us": statistics.median(per[name]), "min_us": min(per[name])}
+            print(kind, {n: round(res[f"{kind}_{n}"]["median_us"], 2) for n, _ in variants}, flush=True)
         alg = bench.lookup_bytes(B * H * W1, L, r)
-        print(json.dumps({"config": a.config, "ldw": ldw, "K": K,
-                          "sheared_MB": sum(t.numel() * 4 for t in S) / 1e6,
-                          "alg_bytes": alg, "results": res}))
+        print(json.dumps({"config": a.config, "K": K, "sheared_MB": sum(t.numel() * 4 for t in S) / 1e6,
+                          "alg_bytes": alg, "bit_identical": True, "results": res}))
 
 
 if __name__ == "__main__":
