@@ -47,7 +47,9 @@ def main():
     B, D, H, W1, W2, L, r, iters, _ = cfg
     dev = torch.device("cuda", 0)
     ll = a.config in bench.LOW_LATENCY_CONFIGS
-    variants = ["exact", "ws"] + [int(m) for m in a.modes.split(",") if m]
+    # "K/M": the split kernel K (RAFTCORR_SPLIT_KERNEL: 8 = the 8-wave kernel)
+    # under mode M; a plain integer M: the 4-wave kernel
+    variants = ["exact", "ws"] + [m if "/" in m else int(m) for m in a.modes.split(",") if m]
     res = {str(v): [] for v in variants}
     with torch.no_grad():
         f1, f2, _ = bench.make_inputs(cfg, dev, seed=1)
@@ -61,17 +63,23 @@ def main():
                 os.environ["RAFTCORR_SPLIT_MODE"] = "0"
                 os.environ["RAFTCORR_SPLIT_KERNEL"] = "3"
                 return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
-            os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
+            if isinstance(v, str):                   # "K/M"
+                kk, mm = v.split("/")
+                os.environ["RAFTCORR_SPLIT_KERNEL"] = kk
+                os.environ["RAFTCORR_SPLIT_MODE"] = mm
+            else:
+                os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
             return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
         ref = None
         for v in variants:
             blk = run(v)()
             if v == 0:
-                ref = [t.clone() for t in blk.corr_pyramid[:1]]
+                ref = [t.clone() for t in blk.corr_pyramid[:4]]
         # schedule variants (128 / 256) must reproduce the product bit for bit
         for v in variants:
-            if isinstance(v, int) and v >= 128 and ref is not None:
-                got = run(v)().corr_pyramid[:1]
+            checked = isinstance(v, str) and not (int(v.split("/")[1]) & 7)   # "K/M" with math and stores
+            if (checked or (isinstance(v, int) and v >= 128)) and ref is not None:
+                got = run(v)().corr_pyramid[:4]
                 res.setdefault("bit_identical", {})[str(v)] = all(
                     bool(torch.equal(x, y)) for x, y in zip(got, ref))
                 res.setdefault("norm_err_vs_0", {})[str(v)] = max(
