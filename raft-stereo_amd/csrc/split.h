@@ -35,8 +35,10 @@ __device__ __forceinline__ float sp_sub(float a, float b) {
 
 // 8 consecutive d of one w -> head, middle and low bf16 pieces (each exact
 // residual of the previous: x = h + m + l for finite |x| < 3.39e38).
-// SCALAR: residuals by sp_sub (v_sub_f32) instead of compiler-packed ops.
-template <bool SCALAR = false>
+// SCALAR (default): residuals by sp_sub (v_sub_f32); false: as the compiler
+// packs them (the dev A/B kModePackedSub; config 2 build 286 vs 280 us,
+// bit-identical, profiles/r04/d/build_ablate.log).
+template <bool SCALAR = true>
 __device__ __forceinline__ SplitFrag sp_split(const float (&x)[8]) {
     u32x4s h, m, l;
     auto sub = [](float a, float b) { return SCALAR ? sp_sub(a, b) : a - b; };

@@ -32,7 +32,7 @@ __device__ __forceinline__ SplitFrag sp_read(const char *base) {
         const bf16x8 hb = __builtin_bit_cast(bf16x8, h);
         return SplitFrag{hb, hb, hb};
     }
-    return sp_split<(MODE & kModeScalarSub) != 0>(x);
+    return sp_split<(MODE & kModePackedSub) == 0>(x);
 }
 
 }  // namespace rc

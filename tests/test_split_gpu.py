@@ -33,6 +33,7 @@ SHAPES = [
     (3, 64, 5, 64, 64),
     (1, 96, 3, 224, 224),       # tiles of 7 fragments: wave blocks of 4 + 3 inside the row
     (1, 64, 2, 96, 176),        # 6 / 11 fragments: tiles of 6 and of 6 + 5
+    (1, 64, 2, 144, 400),       # 9 / 25 fragments: the 8-wave kernel's tiles of 9 and of 13 + 12
 ]
 
 
