@@ -467,7 +467,10 @@ template <int R, int NL, int WPE = 1, bool SEQ = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_bwd_pair_kernel(LookupBwdArgs a) {
     static_assert(NL == 2 || NL == 4, "pair backward: 2 or 4 levels");
     constexpr int NP = NL / 2, T = 2 * R + 1;
-    const long long pblk = (long long)blockIdx.x * 256;
+    // XCD-contiguous block order (as the forward pair kernel): neighbouring
+    // blocks' output-gradient segments share lines at the channel planes'
+    // seams and meet in one XCD's L2
+    const long long pblk = (long long)xcd_remap(blockIdx.x, gridDim.x) * 256;
     const long long p = pblk + threadIdx.x;
     if (p >= a.P) return;   // no barriers in this kernel
     const long long bimg = p / a.HW, rem = p - bimg * a.HW;

@@ -304,7 +304,11 @@ __global__ __launch_bounds__(128) void lookup_bwd_calls_kernel(LookupBwdCallsArg
     constexpr int NP = NL / 2, T = 2 * R + 1;
     float *lds = bwd_calls_lds;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    const long long pblk = (long long)blockIdx.x * a.pix;
+    // XCD-contiguous block order: a call's output-gradient planes start at
+    // multiples of H*W1*4 B (64 mod 128 at config 2), so a block's channel
+    // segments straddle lines its neighbours read too -- on one XCD they meet
+    // in its L2 instead of being fetched by two XCDs
+    const long long pblk = (long long)xcd_remap(blockIdx.x, gridDim.x) * a.pix;
     const int npix = (int)min((long long)a.pix, a.P - pblk);
     for (int f = 4 * tid; f < a.lds_floats; f += 4 * nthr)
         *reinterpret_cast<f32x4 *>(lds + f) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -400,7 +404,7 @@ __global__ __launch_bounds__(64) void lookup_bwd_calls_compact_kernel(LookupBwdC
     float *lds = bwd_calls_lds;
     const int lane = threadIdx.x;
     const int pix = 64 / NP;
-    const long long pblk = (long long)blockIdx.x * pix;
+    const long long pblk = (long long)xcd_remap(blockIdx.x, gridDim.x) * pix;   // see lookup_bwd_calls_kernel
     const int npix = (int)min((long long)pix, a.P - pblk);
     const int k = lane / pix, i = lane - k * pix;
     const bool active = k < NP && i < npix;
