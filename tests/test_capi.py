@@ -193,3 +193,30 @@ def test_build_backward_exact_flag():
     assert bb(_lib.RC_BF16, 0) == _lib.RC_EUNSUPPORTED
     assert bb(_lib.RC_F32 | 0x400000, 0) == _lib.RC_EUNSUPPORTED
     assert L.rc_last_error()
+
+
+def test_backward_entry_points_reject_unknown_flag_bits():
+    """bits of ``levels`` above the level count and the
+    RC_SHADOW_LEVEL byte, other than RC_GRAD_OVERWRITE on
+    rc_corr_lookup_backward_calls, are RC_EINVAL before any launch (they used
+    to be dropped silently)."""
+    L = _lib.lib()
+    f = lambda a: ctypes.c_void_p(a)  # noqa: E731
+    w = _lib.int_array([64, 32, 16, 8])
+    pair = _lib.ptr_array([f(0x1000), None, f(0x2000), None])
+    junk = 4 | 0x100000
+    assert L.rc_corr_lookup_backward(pair, w, None, junk, 4, f(0x7000), 0, 1, 2, 64, f(0x8000),
+                                     None) == _lib.RC_EINVAL
+    assert b"flag" in L.rc_last_error()
+    xs = _lib.ptr_array([f(0x7000)])
+    gos = _lib.ptr_array([f(0x8000)])
+    cbs = _lib.long_array([0])
+    calls = lambda lv: L.rc_corr_lookup_backward_calls(  # noqa: E731
+        pair, w, None, lv, 4, 1, xs, cbs, 1, 2, 64, gos, None)
+    assert calls(junk) == _lib.RC_EINVAL and b"flag" in L.rc_last_error()
+    assert calls(junk | _lib.RC_GRAD_OVERWRITE) == _lib.RC_EINVAL
+    # the documented flag itself is accepted up to the point of validation
+    # (no calls: RC_GRAD_OVERWRITE with n_calls == 0 is its own RC_EINVAL)
+    assert L.rc_corr_lookup_backward_calls(pair, w, None, 4 | _lib.RC_GRAD_OVERWRITE, 4, 0, None, None,
+                                           1, 2, 64, None, None) == _lib.RC_EINVAL
+    assert b"no calls" in L.rc_last_error()
