@@ -77,7 +77,7 @@ def main():
                 ref = [t.clone() for t in blk.corr_pyramid[:4]]
         # schedule variants (128 / 256) must reproduce the product bit for bit
         for v in variants:
-            checked = isinstance(v, str) and not (int(v.split("/")[1]) & 7)   # "K/M" with math and stores
+            checked = isinstance(v, str) and "/" in v and not (int(v.split("/")[1]) & 7)   # "K/M", math + stores
             if (checked or (isinstance(v, int) and v >= 128)) and ref is not None:
                 got = run(v)().corr_pyramid[:4]
                 res.setdefault("bit_identical", {})[str(v)] = all(
