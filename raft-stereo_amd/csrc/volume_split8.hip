@@ -5,6 +5,10 @@
 // and the avg_pool2d loop of CorrBlock1D.__init__ (:284-295).
 #include "split_ring.h"
 
+// DEV LIBRARY ONLY (RAFTCORR_SPLIT_KERNEL=8): measured and not kept -- config 2
+// 309 vs 277 us for build_split_kernel, compute alone 193 vs 189 us
+// (profiles/r04/f/build_ablate.log); Middlebury 1061 vs 1128.
+#ifdef RAFTCORR_DEV
 namespace rc {
 
 // ====== 8-wave variant: 64 x 128 wave tiles, one workgroup per 256 x 256 tile ======
@@ -167,11 +171,17 @@ __global__ __launch_bounds__(512, 1) void build_split8_kernel(BuildArgs a, int n
 }
 
 }  // namespace rc
+#endif  // RAFTCORR_DEV
 
 // Launches the 8-wave kernel when it applies (tiles of >= 9 fragments along
 // both widths, i.e. W1, W2 >= 129, and the launcher's choice); otherwise
 // returns hipErrorNotSupported and launches nothing.
 hipError_t rc_launch_build_split8(const rc::BuildArgs &a, hipStream_t s) {
+#ifndef RAFTCORR_DEV
+    (void)a;
+    (void)s;
+    return hipErrorNotSupported;
+#else
     // 8-wave kernel: tiles of up to 16 x 16 fragments, balanced like the
     // 4-wave kernel's (W = 240: one 15-fragment tile; W = 720: three)
     auto tile16 = [](int W) {
@@ -212,4 +222,5 @@ hipError_t rc_launch_build_split8(const rc::BuildArgs &a, hipStream_t s) {
         return hipGetLastError();
     }
     return hipErrorNotSupported;
+#endif
 }
