@@ -84,6 +84,14 @@ if has pmcw; then   # wave-state breakdown: where each kernel's wave cycles go
         --output-format csv -d "$OUT/pmc_w2" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
     python tools/pmc_raw.py "$OUT/pmc_w1" > "$OUT/pmc_w.txt" 2>&1; python tools/pmc_raw.py "$OUT/pmc_w2" >> "$OUT/pmc_w.txt" 2>&1; grep lookup "$OUT/pmc_w.txt"
 fi
+if has pmcs8; then   # split kernels (4- vs 8-wave, product vs compute-only): instruction mix and wave states
+    BA8="--modes ${PMCS8_MODES:-0,3,8/0,8/3} --rounds 1 --per 3"
+    step pmc_s81 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE \
+        --output-format csv -d "$OUT/pmc_s81" -o s -- python3 tools/build_ablate.py $BA8
+    step pmc_s82 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
+        --output-format csv -d "$OUT/pmc_s82" -o s -- python3 tools/build_ablate.py $BA8
+    python tools/pmc_raw.py "$OUT/pmc_s81" > "$OUT/pmc_s8.txt" 2>&1; python tools/pmc_raw.py "$OUT/pmc_s82" >> "$OUT/pmc_s8.txt" 2>&1; grep split "$OUT/pmc_s8.txt"
+fi
 if has pmcv; then
     step pmc_v1 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_VMEM_TA_ADDR_FIFO_FULL SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
         --output-format csv -d "$OUT/pmc_v1" -o s -- python3 tools/probe.py ${PROBE_ARGS:-}
