@@ -118,6 +118,7 @@ fi
 has shard8 && step shard_probe_h8 900 python tools/shard_probe.py --halo 8
 has sabl && step build_ablate 600 python tools/build_ablate.py --modes ${SABL_MODES:-0,8192} --rounds ${SABL_ROUNDS:-9} ${SABL_CONFIG:+--config $SABL_CONFIG}
 has shear && step shear_probe 600 python tools/shear_probe.py
+has gfloor && step graph_floor 300 python tools/graph_floor.py
 has train && step train_probe 300 python tools/train_probe.py
 has lprobe2 && step lookup_probe2 600 python tools/lookup_probe.py --only-dev --dev-variants ${LPROBE_VARIANTS:-215} --dev-fields ${LPROBE_FIELDS:-bench,smooth,net} --reps ${LPROBE_REPS:-7}
 if has calib; then   # FETCH_SIZE / WRITE_SIZE per byte for scattered 64-256 B rows
