@@ -14,7 +14,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8, kModeNoFragReads = 16,
        kModeStagger = 64, kModeSched = 128, kModeReorder = 256,
        kModeNoMfma = 512, kModeNoSplit = 1024, kModeSpread = 2048, kModePackedSub = 8192,
-       kMode32 = 16384 };
+       kMode32 = 16384, kModePhase = 32768 };
 
 // VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
 template <int VW>

@@ -152,7 +152,23 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
                 sp_mma6(c, x, y);
             };
             SplitFrag fb[FB];
-            if constexpr (MODE & (kModeSched | kModeReorder)) {
+            if constexpr (MODE & kModePhase) {
+                // phased order (dev A/B): every fragment of the K step read and
+                // split first, then all the MFMAs -- a wave alternates a VALU
+                // phase and an MFMA phase, and its SIMD partner (the other
+                // workgroup's wave) can fill one with the other.  Same products,
+                // same order per accumulator: bit-identical.
+                SplitFrag fas[FA];
+#pragma unroll
+                for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE>(pb + 64 * n);
+#pragma unroll
+                for (int m = 0; m < FA; ++m) fas[m] = sp_read<MODE>(pa + 64 * m);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < FA; ++m)
+#pragma unroll
+                    for (int n = 0; n < FB; ++n) mma6(acc[m][n], fas[m], fb[n]);
+            } else if constexpr (MODE & (kModeSched | kModeReorder)) {
                 // pipelined order (dev A/B): only A0 and B0 are split before
                 // the first MFMA; B1.. are split while the MFMAs of A0 run,
                 // A(m+1) while those of A(m) run.  Same products, same
@@ -613,6 +629,8 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         case 8192: hipLaunchKernelGGL((rc::build_split_kernel<8192, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 16384: hipLaunchKernelGGL((rc::build_split_kernel<16384, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 24576: hipLaunchKernelGGL((rc::build_split_kernel<24576, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 32768: hipLaunchKernelGGL((rc::build_split_kernel<32768, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 32771: hipLaunchKernelGGL((rc::build_split_kernel<32771, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         default: break;
     }
 #endif
