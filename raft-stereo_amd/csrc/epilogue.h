@@ -14,7 +14,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8, kModeNoFragReads = 16,
        kModeStagger = 64, kModeSched = 128, kModeReorder = 256,
        kModeNoMfma = 512, kModeNoSplit = 1024, kModeSpread = 2048, kModePackedSub = 8192,
-       kMode32 = 16384, kModePhase = 32768 };
+       kMode32 = 16384, kModePhase = 32768, kModeL2Stores = 65536,
+       kModeDirect = 131072, kModeFastEpi = 262144, kModeGenericEpi = 524288 };
 
 // VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
 template <int VW>
@@ -135,6 +136,56 @@ __device__ __forceinline__ float pool2(float x, float y, bool bf) {
     return bf ? round_bf16(m) : m;
 }
 
+// Rows [0, 16) of a wave's staged fp32 image of level L (CW columns, a
+// multiple of VW, pitch CW + 4 floats) -> level memory as VW-float vectors,
+// with the geometry known at compile time: every LDS read of the flush
+// issued before one wait, then the stores (store_rows16's loop waits once per
+// row group and divides by runtime widths).
+template <int VW> struct FlushVec;
+template <> struct FlushVec<4> { typedef f32x4 T; };
+template <> struct FlushVec<2> { typedef f32x2 T; };
+template <> struct FlushVec<1> { typedef float T; };
+
+template <int CW, int L, int VW>
+__device__ __forceinline__ void flush_rows16_fast(uint32_t st, const BuildArgs &a, long long rowbase, int w1_0,
+                                                  int n0, int w1e, int lane) {
+    static_assert(CW % VW == 0, "whole vectors per row");
+    typedef typename FlushVec<VW>::T V;
+    constexpr int LP = CW / VW;                // lanes per row
+    constexpr int RPI = 64 / LP;               // rows per instruction
+    constexpr int NI = (16 + RPI - 1) / RPI;   // instructions
+    const int Rl = lane / LP, j = (lane - Rl * LP) * VW;
+    const int col = (n0 >> L) + j;
+    const bool lok = Rl < RPI && col < (a.W2 >> L);
+    V x[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int R = k * RPI + Rl;
+        const uint32_t src = st + 4 * ((R < 16 ? R : 15) * (CW + 4) + j);
+        if constexpr (VW == 4) asm volatile("ds_read_b128 %0, %1" : "=v"(x[k]) : "v"(src));
+        else if constexpr (VW == 2) asm volatile("ds_read_b64 %0, %1" : "=v"(x[k]) : "v"(src));
+        else asm volatile("ds_read_b32 %0, %1" : "=v"(x[k]) : "v"(src));
+    }
+    // the wait names the read registers, so no use of them moves above it
+    static_assert(NI == 1 || NI == 2 || NI == 4, "flush instruction count");
+    if constexpr (NI == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0])::"memory");
+    else if constexpr (NI == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0]), "+v"(x[1])::"memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3])::"memory");
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int R = k * RPI + Rl, w1 = w1_0 + R;
+        if (lok && R < 16 && w1 < w1e) {
+            float v[VW];
+            if constexpr (VW == 1) v[0] = x[k];
+            else {
+#pragma unroll
+                for (int c = 0; c < VW; ++c) v[c] = x[k][c];
+            }
+            store_vec<VW>(a.lvl[L], false, (rowbase + w1) * a.ld[L] + col, v, a.shadow[L]);
+        }
+    }
+}
+
 // Epilogue of the swapped-operand tile: acc[ma][nb] register r of lane l =
 // C[w1 = m0 + 16nb + (l&15)][w2 = n0 + 16ma + 4(l>>4) + r].  One fragment
 // column nb (16 w1 rows) at a time, every level: level l's image has rows
@@ -148,8 +199,143 @@ __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const Bui
     const int w1e = w1_end < 0 || w1_end > a.W1 ? a.W1 : w1_end;
     constexpr int WT = 16 * FMA;
     const bool bf = a.pyr_bf16 != 0;
-    const long long rowbase = (long long)row * a.W1;
+    // kModeL2Stores (dev timing only, wrong output): every row stores into
+    // one of 8 rows, so the same instructions write L2-resident lines
+    const long long rowbase = (long long)((MODE & kModeL2Stores) ? (row & 7) : row) * a.W1;
     const int nl = a.nfused < NLM ? a.nfused : NLM;
+    if constexpr ((MODE & kModeFastEpi) != 0 && (MODE & (kModeNoStores | kModeL2Stores | kModeDirect)) == 0) {
+        // fp32 levels 0-2, power-of-two scale, 16-B aligned rows: the
+        // geometry of every flush is compile-time (flush_rows16_fast)
+        const bool fast = !bf && a.pow2 && (!a.lvl[0] || a.ld[0] % 4 == 0) &&
+                          (nl < 2 || !a.lvl[1] || a.ld[1] % 4 == 0) && (nl < 3 || !a.lvl[2] || a.ld[2] % 4 == 0) &&
+                          (nl < 4 || !a.lvl[3] || a.ld[3] % 2 == 0);
+        if (fast) {
+            const int g = lane0 >> 4, i = lane0 & 15;
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                float v[FMA][4];
+#pragma unroll
+                for (int ma = 0; ma < FMA; ++ma)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[ma][r] = acc[ma][nb][r] * a.scale;
+                const int w1_0 = m0 + 16 * nb;
+                if (a.lvl[0]) {
+#pragma unroll
+                    for (int ma = 0; ma < FMA; ++ma)
+                        lds_st4(st0 + 4 * (i * (WT + 4) + 16 * ma + 4 * g), f32x4{v[ma][0], v[ma][1], v[ma][2], v[ma][3]});
+                    flush_rows16_fast<WT, 0, 4>(st0, a, rowbase, w1_0, n0, w1e, lane0);
+                }
+                if (nl < 2) continue;
+                float u[FMA][2];
+#pragma unroll
+                for (int ma = 0; ma < FMA; ++ma) {
+                    u[ma][0] = pool2(v[ma][0], v[ma][1], false);
+                    u[ma][1] = pool2(v[ma][2], v[ma][3], false);
+                }
+                if (a.lvl[1]) {
+#pragma unroll
+                    for (int ma = 0; ma < FMA; ++ma)
+                        lds_st2(st0 + 4 * (i * (WT / 2 + 4) + 8 * ma + 2 * g), f32x2{u[ma][0], u[ma][1]});
+                    flush_rows16_fast<WT / 2, 1, 4>(st0, a, rowbase, w1_0, n0, w1e, lane0);
+                }
+                if (nl < 3) continue;
+                float s2[FMA];
+#pragma unroll
+                for (int ma = 0; ma < FMA; ++ma) s2[ma] = pool2(u[ma][0], u[ma][1], false);
+                if (a.lvl[2]) {
+#pragma unroll
+                    for (int ma = 0; ma < FMA; ++ma) lds_st1(st0 + 4 * (i * (WT / 4 + 4) + 4 * ma + g), s2[ma]);
+                    flush_rows16_fast<WT / 4, 2, 4>(st0, a, rowbase, w1_0, n0, w1e, lane0);
+                }
+                if constexpr (NLM >= 4) {
+                    if (nl < 4) continue;
+                    // level 3: lanes l, l^16; level 4: lanes l, l^32 (as below)
+                    float s3[FMA];
+#pragma unroll
+                    for (int ma = 0; ma < FMA; ++ma) {
+                        const float o = __shfl_xor(s2[ma], 16);
+                        s3[ma] = (g & 1) ? pool2(o, s2[ma], false) : pool2(s2[ma], o, false);
+                    }
+                    if (a.lvl[3]) {
+                        if (!(g & 1)) {
+#pragma unroll
+                            for (int ma = 0; ma < FMA; ++ma)
+                                lds_st1(st0 + 4 * (i * (WT / 8 + 4) + 2 * ma + (g >> 1)), s3[ma]);
+                        }
+                        flush_rows16_fast<WT / 8, 3, 2>(st0, a, rowbase, w1_0, n0, w1e, lane0);
+                    }
+                    if constexpr (NLM >= 5) {
+                        if (nl < 5) continue;
+                        float s4[FMA];
+#pragma unroll
+                        for (int ma = 0; ma < FMA; ++ma) {
+                            const float o = __shfl_xor(s3[ma], 32);
+                            s4[ma] = (g & 2) ? pool2(o, s3[ma], false) : pool2(s3[ma], o, false);
+                        }
+                        if (a.lvl[4]) {
+                            if (g == 0) {
+#pragma unroll
+                                for (int ma = 0; ma < FMA; ++ma) lds_st1(st0 + 4 * (i * (WT / 16 + 4) + ma), s4[ma]);
+                            }
+                            flush_rows16_fast<WT / 16, 4, 1>(st0, a, rowbase, w1_0, n0, w1e, lane0);
+                        }
+                    }
+                }
+            }
+            return;
+        }
+    }
+    if constexpr ((MODE & kModeDirect) != 0) {
+        // each lane stores its own values straight from the registers (no
+        // LDS image): level l of lane (i, g) for fragment (ma, nb) is row
+        // w1 = m0 + 16nb + i, columns ((n0 + 16ma + 4g) >> l) .. +(4 >> l)
+        const int g = lane0 >> 4, i = lane0 & 15;
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+            const int w1 = m0 + 16 * nb + i;
+            const bool rok = w1 < w1e;
+            const long long rb = rowbase + w1;
+            float v[FMA][4];
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float x = acc[ma][nb][r];
+                    const float c = a.pow2 ? x * a.scale : x / a.sq;
+                    v[ma][r] = bf ? round_bf16(c) : c;
+                }
+            auto put = [&](int l, int col, const float *x, int n) {   // n consecutive values of level l
+                if (!a.lvl[l] || !rok || col >= (a.W2 >> l)) return;
+                const long long e = rb * a.ld[l] + col;
+                if (n == 4 && a.ld[l] % 4 == 0) store_vec<4>(a.lvl[l], bf, e, x, a.shadow[l]);
+                else if (n >= 2 && a.ld[l] % 2 == 0) {
+                    store_vec<2>(a.lvl[l], bf, e, x, a.shadow[l]);
+                    if (n == 4) store_vec<2>(a.lvl[l], bf, e + 2, x + 2, a.shadow[l]);
+                } else {
+                    for (int k = 0; k < n; ++k) store_vec<1>(a.lvl[l], bf, e + k, x + k, a.shadow[l]);
+                }
+            };
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma) {
+                put(0, n0 + 16 * ma + 4 * g, v[ma], 4);
+                if (nl < 2) continue;
+                const float u[2] = {pool2(v[ma][0], v[ma][1], bf), pool2(v[ma][2], v[ma][3], bf)};
+                put(1, (n0 >> 1) + 8 * ma + 2 * g, u, 2);
+                if (nl < 3) continue;
+                const float s2 = pool2(u[0], u[1], bf);
+                put(2, (n0 >> 2) + 4 * ma + g, &s2, 1);
+                if (nl < 4) continue;
+                const float o3 = __shfl_xor(s2, 16);
+                const float s3 = (g & 1) ? pool2(o3, s2, bf) : pool2(s2, o3, bf);
+                if (!(g & 1)) put(3, (n0 >> 3) + 2 * ma + (g >> 1), &s3, 1);
+                if (nl < 5) continue;
+                const float o4 = __shfl_xor(s3, 32);
+                const float s4 = (g & 2) ? pool2(o4, s3, bf) : pool2(s3, o4, bf);
+                if (g == 0) put(4, (n0 >> 4) + ma, &s4, 1);
+            }
+        }
+        return;
+    }
     // one loop body for the four columns (code size, registers): column nb
     // is always acc[.][0], the others move down one per pass
 #pragma unroll 1

@@ -240,8 +240,12 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if constexpr (FA > 0)
-        epilogue_swapped<FA, MODE, NLM>(acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
-                                        lds_u32(smem + c.wave * kSpStb), c.M0 + c.o1 + 16 * FB);
+        // the compile-time-geometry flushes (fp32 levels 0-2) unless the dev
+        // A/B asks for the generic epilogue: config 2 262.5 vs 281.2 us
+        // (profiles/r04/o/build_ablate.log, bit-identical)
+        epilogue_swapped<FA, (MODE & kModeGenericEpi) ? MODE : (MODE | kModeFastEpi), NLM>(
+            acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
+            lds_u32(smem + c.wave * kSpStb), c.M0 + c.o1 + 16 * FB);
 }
 
 template <int FA, int MODE, int NLM>
@@ -618,6 +622,8 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         case 2: hipLaunchKernelGGL((rc::build_split_kernel<2, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 3: hipLaunchKernelGGL((rc::build_split_kernel<3, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 4: hipLaunchKernelGGL((rc::build_split_kernel<4, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 5: hipLaunchKernelGGL((rc::build_split_kernel<5, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 65541: hipLaunchKernelGGL((rc::build_split_kernel<65541, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 6: hipLaunchKernelGGL((rc::build_split_kernel<6, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 7: hipLaunchKernelGGL((rc::build_split_kernel<7, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 128: hipLaunchKernelGGL((rc::build_split_kernel<128, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
@@ -630,6 +636,13 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         case 16384: hipLaunchKernelGGL((rc::build_split_kernel<16384, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 24576: hipLaunchKernelGGL((rc::build_split_kernel<24576, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 32768: hipLaunchKernelGGL((rc::build_split_kernel<32768, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 524288: hipLaunchKernelGGL((rc::build_split_kernel<524288, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 524293: hipLaunchKernelGGL((rc::build_split_kernel<524288, rc::kSpMaxFused>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 262144: hipLaunchKernelGGL((rc::build_split_kernel<262144, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 262149: hipLaunchKernelGGL((rc::build_split_kernel<262149, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 131072: hipLaunchKernelGGL((rc::build_split_kernel<131072, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 131077: hipLaunchKernelGGL((rc::build_split_kernel<131072, rc::kSpMaxFused>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 65536: hipLaunchKernelGGL((rc::build_split_kernel<65536, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 32771: hipLaunchKernelGGL((rc::build_split_kernel<32771, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         default: break;
     }
