@@ -189,6 +189,8 @@ struct BuildBwdArgs {
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s);
 hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s);     // may lower a.nfused
 hipError_t rc_launch_build_split8(const rc::BuildArgs &a, hipStream_t s);   // hipErrorNotSupported: not taken
+hipError_t rc_launch_build_split_persist(const rc::BuildArgs &a, long long ntiles, int tf1, int tf2, int tiles1,
+                                         int tiles2, hipStream_t s);   // hipErrorNotSupported: not taken
 hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s);   // may lower a.nfused
 hipError_t rc_launch_pool(const void *in, long long ld_in, void *out, long long ld_out, long rows,
                           int W_in, int bf16, hipStream_t s);

@@ -615,6 +615,14 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         if (e8 != hipErrorNotSupported) return e8;
     }
 #ifdef RAFTCORR_DEV
+    // dev-only: RAFTCORR_SPLIT_KERNEL=4 runs the persistent deferred-epilogue
+    // kernel (volume_split_p.hip) where it applies
+    if (rc::dev_knob("RAFTCORR_SPLIT_KERNEL") == 4) {
+        const hipError_t ep = rc_launch_build_split_persist(a, nwg, tf1, tf2, tiles1, tiles2, s);
+        if (ep != hipErrorNotSupported) return ep;
+    }
+#endif
+#ifdef RAFTCORR_DEV
     // dev-only ablations (timing only): RAFTCORR_SPLIT_MODE = kMode* flags
     // (1 no operand loads, 2 no epilogue stores, 4 no MFMAs; sums combine)
     switch (rc::dev_knob("RAFTCORR_SPLIT_MODE")) {
