@@ -15,7 +15,8 @@ enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8
        kModeStagger = 64, kModeSched = 128, kModeReorder = 256,
        kModeNoMfma = 512, kModeNoSplit = 1024, kModeSpread = 2048, kModePackedSub = 8192,
        kMode32 = 16384, kModePhase = 32768, kModeL2Stores = 65536,
-       kModeDirect = 131072, kModeFastEpi = 262144, kModeGenericEpi = 524288 };
+       kModeDirect = 131072, kModeFastEpi = 262144, kModeGenericEpi = 524288,
+       kModePairEpi = 1048576 };
 
 // VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
 template <int VW>
@@ -186,6 +187,49 @@ __device__ __forceinline__ void flush_rows16_fast(uint32_t st, const BuildArgs &
     }
 }
 
+// The same flush split in two, so that several images' reads share one
+// wait: flush_issue (LDS reads of rows [0, 16) of a staged image) and
+// flush_store (their stores), with flush_settle between them.
+template <int CW, int L>
+struct FlushRegs {
+    static constexpr int LP = CW / 4, RPI = 64 / LP, NI = (16 + RPI - 1) / RPI;
+    f32x4 x[NI];
+};
+template <int CW, int L>
+__device__ __forceinline__ void flush_issue(FlushRegs<CW, L> &f, uint32_t st, int lane) {
+    typedef FlushRegs<CW, L> F;
+    const int Rl = lane / F::LP, j = (lane - Rl * F::LP) * 4;
+#pragma unroll
+    for (int k = 0; k < F::NI; ++k) {
+        const int R = k * F::RPI + Rl;
+        const uint32_t src = st + 4 * ((R < 16 ? R : 15) * (CW + 4) + j);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(f.x[k]) : "v"(src));
+    }
+}
+// after the shared wait: the registers pass through an asm that follows it,
+// so no use of them moves above the wait
+template <int CW, int L>
+__device__ __forceinline__ void flush_settle(FlushRegs<CW, L> &f) {
+#pragma unroll
+    for (int k = 0; k < FlushRegs<CW, L>::NI; ++k) asm volatile("" : "+v"(f.x[k]));
+}
+template <int CW, int L>
+__device__ __forceinline__ void flush_store(const FlushRegs<CW, L> &f, const BuildArgs &a, long long rowbase,
+                                            int w1_0, int n0, int w1e, int lane) {
+    typedef FlushRegs<CW, L> F;
+    const int Rl = lane / F::LP, j = (lane - Rl * F::LP) * 4;
+    const int col = (n0 >> L) + j;
+    const bool lok = Rl < F::RPI && col < (a.W2 >> L);
+#pragma unroll
+    for (int k = 0; k < F::NI; ++k) {
+        const int R = k * F::RPI + Rl, w1 = w1_0 + R;
+        if (lok && R < 16 && w1 < w1e) {
+            const float v[4] = {f.x[k][0], f.x[k][1], f.x[k][2], f.x[k][3]};
+            store_vec<4>(a.lvl[L], false, (rowbase + w1) * a.ld[L] + col, v, a.shadow[L]);
+        }
+    }
+}
+
 // Epilogue of the swapped-operand tile: acc[ma][nb] register r of lane l =
 // C[w1 = m0 + 16nb + (l&15)][w2 = n0 + 16ma + 4(l>>4) + r].  One fragment
 // column nb (16 w1 rows) at a time, every level: level l's image has rows
@@ -209,6 +253,73 @@ __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const Bui
         const bool fast = !bf && a.pow2 && (!a.lvl[0] || a.ld[0] % 4 == 0) &&
                           (nl < 2 || !a.lvl[1] || a.ld[1] % 4 == 0) && (nl < 3 || !a.lvl[2] || a.ld[2] % 4 == 0) &&
                           (nl < 4 || !a.lvl[3] || a.ld[3] % 2 == 0);
+        if constexpr (NLM <= 3 && (MODE & kModePairEpi) != 0) {
+            if (fast) {
+                // two fragment columns at a time: every level image of both
+                // staged in its own region of the wave's 16 KB of the ring,
+                // all their reads, ONE wait, then all their stores
+                const int g = lane0 >> 4, i = lane0 & 15;
+                constexpr int S0 = 16 * (WT + 4) * 4, S1 = 16 * (WT / 2 + 4) * 4, S2 = 16 * (WT / 4 + 4) * 4;
+                constexpr int SNB = S0 + S1 + S2;
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    FlushRegs<WT, 0> r0[2];
+                    FlushRegs<WT / 2, 1> r1[2];
+                    FlushRegs<WT / 4, 2> r2[2];
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int nb = 2 * p + k;
+                        const uint32_t b = st0 + k * SNB;
+                        float v[FMA][4];
+#pragma unroll
+                        for (int ma = 0; ma < FMA; ++ma)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) v[ma][r] = acc[ma][nb][r] * a.scale;
+                        if (a.lvl[0]) {
+#pragma unroll
+                            for (int ma = 0; ma < FMA; ++ma)
+                                lds_st4(b + 4 * (i * (WT + 4) + 16 * ma + 4 * g), f32x4{v[ma][0], v[ma][1], v[ma][2], v[ma][3]});
+                            flush_issue(r0[k], b, lane0);
+                        }
+                        if (nl < 2) continue;
+                        float u[FMA][2];
+#pragma unroll
+                        for (int ma = 0; ma < FMA; ++ma) {
+                            u[ma][0] = pool2(v[ma][0], v[ma][1], false);
+                            u[ma][1] = pool2(v[ma][2], v[ma][3], false);
+                        }
+                        if (a.lvl[1]) {
+#pragma unroll
+                            for (int ma = 0; ma < FMA; ++ma)
+                                lds_st2(b + S0 + 4 * (i * (WT / 2 + 4) + 8 * ma + 2 * g), f32x2{u[ma][0], u[ma][1]});
+                            flush_issue(r1[k], b + S0, lane0);
+                        }
+                        if (nl < 3) continue;
+                        if (a.lvl[2]) {
+#pragma unroll
+                            for (int ma = 0; ma < FMA; ++ma)
+                                lds_st1(b + S0 + S1 + 4 * (i * (WT / 4 + 4) + 4 * ma + g), pool2(u[ma][0], u[ma][1], false));
+                            flush_issue(r2[k], b + S0 + S1, lane0);
+                        }
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        flush_settle(r0[k]);
+                        flush_settle(r1[k]);
+                        flush_settle(r2[k]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int w1_0 = m0 + 16 * (2 * p + k);
+                        if (a.lvl[0]) flush_store(r0[k], a, rowbase, w1_0, n0, w1e, lane0);
+                        if (nl >= 2 && a.lvl[1]) flush_store(r1[k], a, rowbase, w1_0, n0, w1e, lane0);
+                        if (nl >= 3 && a.lvl[2]) flush_store(r2[k], a, rowbase, w1_0, n0, w1e, lane0);
+                    }
+                }
+                return;
+            }
+        }
         if (fast) {
             const int g = lane0 >> 4, i = lane0 & 15;
 #pragma unroll

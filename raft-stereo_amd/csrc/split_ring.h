@@ -16,6 +16,8 @@ constexpr int kSpSL = 4;                    // ring slots (stages): one K step i
 constexpr int kSpMaxFused = 5;              // levels the epilogue writes (more: pooled from memory)
 constexpr int kSpStb = 16 * (64 + 4) * 4;   // per-wave epilogue staging (epilogue_swapped, WT 64)
 static_assert(4 * kSpStb <= kSpSL * kSpSlot, "epilogue staging aliases the ring");
+// the pair epilogue (kModePairEpi): two columns of levels 0-2 per wave, at WT = 64
+static_assert(2 * 16 * ((64 + 4) + (32 + 4) + (16 + 4)) * 4 <= kSpSL * kSpSlot / 4, "pair staging per wave");
 
 // One lane's fragment: rows r0..r0+7 (d inside the stage) of w column w of an
 // operand tile at LDS byte address base.  Row d of the tile sits in block

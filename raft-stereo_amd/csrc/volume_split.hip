@@ -245,7 +245,7 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
         // (profiles/r04/o/build_ablate.log, bit-identical)
         epilogue_swapped<FA, (MODE & kModeGenericEpi) ? MODE : (MODE | kModeFastEpi), NLM>(
             acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
-            lds_u32(smem + c.wave * kSpStb), c.M0 + c.o1 + 16 * FB);
+            lds_u32(smem + c.wave * (kSpSL * kSpSlot / 4)), c.M0 + c.o1 + 16 * FB);
 }
 
 template <int FA, int MODE, int NLM>
@@ -644,6 +644,7 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         case 16384: hipLaunchKernelGGL((rc::build_split_kernel<16384, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 24576: hipLaunchKernelGGL((rc::build_split_kernel<24576, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 32768: hipLaunchKernelGGL((rc::build_split_kernel<32768, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 1048576: hipLaunchKernelGGL((rc::build_split_kernel<1048576, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 524288: hipLaunchKernelGGL((rc::build_split_kernel<524288, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 524293: hipLaunchKernelGGL((rc::build_split_kernel<524288, rc::kSpMaxFused>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 262144: hipLaunchKernelGGL((rc::build_split_kernel<262144, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
