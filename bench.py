@@ -714,7 +714,8 @@ def main():
                   "writes are in the build's time, not in its algorithmic bytes); every lookup "
                   "recomputes the others from them bit-exactly (rc_corr_lookup_chain); the rest "
                   "are materialised only when corr_pyramid is read" if blk._chain else
-                  "the build writes all num_levels+1 pyramid levels"),
+                  f"per-level lookup: the build writes the levels a lookup reads, {written}; "
+                  "level num_levels is pooled only when corr_pyramid is read"),
     }
     if not args.no_backward and args.config == "sceneflow":
         result["backward"] = backward_timing(cfg, f1, f2, coords)

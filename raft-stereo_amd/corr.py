@@ -671,8 +671,8 @@ class CorrBlock1D:
         self._chain = (1 <= radius <= 4 and fmap2.shape[-1] <= 65536 and
                        (num_levels in (2, 3, 4) if pyramid_dtype == torch.float32 else
                         num_levels in (2, 4) if pyramid_dtype == torch.bfloat16 else False))
-        # low_latency (small inputs, e.g. the realtime config): store every
-        # level and use the per-level lookup, whose launcher gives each level
+        # low_latency (small inputs, e.g. the realtime config): store the
+        # levels a lookup reads and use the per-level lookup, whose launcher gives each level
         # its own wave below 64K pixels (lookup_levelpar_kernel, DESIGN.md
         # §3.2g): a shorter dependent chain per launch, bit-identical values
         # grad_shadow: levels (0, 2 of the 4-level pair layout) whose gradient
@@ -688,6 +688,11 @@ class CorrBlock1D:
                 nbuf, skip = 2, ()
             elif lazy:
                 nbuf, skip = (1, ()) if num_levels == 2 else (3, (1,))
+            elif lazy_levels is None or lazy_levels:
+                # per-level lookup (low_latency, or no pool chain): levels
+                # 0 .. L-1 are read (model.py:303-304); level L, which no
+                # lookup reads, is pooled when corr_pyramid is read
+                nbuf, skip = num_levels, ()
             else:
                 nbuf, skip = num_levels + 1, ()
             # RC_SHADOW: stored levels of the pair layout may
@@ -743,11 +748,19 @@ class CorrBlock1D:
         self._chain = False
         self._shadow = frozenset()
 
+    def _read_levels(self):
+        """Levels 0 .. num_levels-1 for the per-level kernels (the ones a
+        lookup reads), without materialising a lazily pooled top level."""
+        L = self.num_levels
+        if all(t is not None for t in self._levels[:L]):
+            return self._levels[:L]
+        return self.corr_pyramid[:L]
+
     def _lookup(self, coords):
         if self._chain:
             return lookup_chain(self._levels, coords, self.num_levels, self.radius, self._shadow,
                                 self.channels_last)
-        out = lookup(self.corr_pyramid, coords, self.num_levels, self.radius)
+        out = lookup(self._read_levels(), coords, self.num_levels, self.radius)
         return out.contiguous(memory_format=torch.channels_last) if self.channels_last else out
 
     def __call__(self, coords):
@@ -794,7 +807,7 @@ class CorrBlock1D:
         if self._chain:
             keep, ptrs, widths, lds, dt = _chain_args(self._levels, L, self._shadow)
         else:
-            keep, ptrs, widths, lds, dt = _level_args(self.corr_pyramid, L)
+            keep, ptrs, widths, lds, dt = _level_args(self._read_levels(), L)
         if cl:
             dt |= _lib.RC_OUT_CHANNELS_LAST
         with torch.cuda.device(c1.device):
@@ -815,7 +828,7 @@ class CorrBlock1D:
         if torch.is_grad_enabled() and (self._token is not None or weight.requires_grad):
             raise RuntimeError("CorrBlock1D.lookup_convc1 is inference-only; use "
                                "convc1(block(coords)) when gradients are needed")
-        return lookup_convc1(self.corr_pyramid, coords, self.num_levels, self.radius, weight,
+        return lookup_convc1(self._read_levels(), coords, self.num_levels, self.radius, weight,
                              bias, relu)
 
     @staticmethod

@@ -1,5 +1,6 @@
-"""CorrBlock1D(low_latency=True): every level stored, per-level lookup that
-gives each level its own wave below 64K pixels (lookup_levelpar_kernel).
+"""CorrBlock1D(low_latency=True): the levels a lookup reads (0 .. L-1) stored,
+the top one pooled when corr_pyramid is read; per-level lookup that gives
+each level its own wave below 64K pixels (lookup_levelpar_kernel).
 Same values bit for bit as the default block (pair / chain kernels), incl.
 NaN/inf/subnormal coords and the fused loop step updating coords in place
 (the kernel's block barrier orders the coords reads before the writes)."""
@@ -28,8 +29,9 @@ def test_low_latency_bit_identical(shape, dt):
     with torch.no_grad():
         ref = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=dt)
         ll = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=dt, low_latency=True)
-        assert not ll._chain and ll.levels_stored == list(range(L + 1))
+        assert not ll._chain and ll.levels_stored == list(range(L))
         assert torch.equal(ll(coords).view(torch.int32), ref(coords).view(torch.int32))
+        assert ll.levels_stored == list(range(L))       # the lookup did not pool the top level
         d = torch.randn(coords.shape, generator=g).to(DEV)
         c_ref, c_ll = coords.clone(), coords.clone()
         a = ref.lookup_step(c_ref, d, out=c_ref)        # in place
@@ -37,6 +39,16 @@ def test_low_latency_bit_identical(shape, dt):
         for u, v in zip(a, b):
             assert torch.equal(u.view(torch.int32), v.view(torch.int32))
         assert torch.equal(c_ref.view(torch.int32), c_ll.view(torch.int32))
+        # every level, the lazily pooled top one included, equals the default
+        # block's (and the eager build's) bit for bit
+        eager = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=dt, low_latency=True,
+                            lazy_levels=False)
+        assert eager.levels_stored == list(range(L + 1))
+        iv = torch.int16 if dt == torch.bfloat16 else torch.int32
+        for u, v, w in zip(ref.corr_pyramid, ll.corr_pyramid, eager.corr_pyramid):
+            assert torch.equal(u.contiguous().view(iv), v.contiguous().view(iv))
+            assert torch.equal(v.contiguous().view(iv), w.contiguous().view(iv))
+        assert len(ll.corr_pyramid) == L + 1
 
 
 # below 64K pixels every rc_corr_lookup with 1-4 levels takes the
