@@ -829,7 +829,8 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             // level 2 is small (8 B per lane and column): stored right away
             const int w1 = m0h + 16 * nb + i16, col = (n0h >> 2) + 4 * g;
             if (!(MODE & kModeNoStores) && w1 < W1 && col < (W2 >> 2)) {
-                uint16_t *d = reinterpret_cast<uint16_t *>(a.lvl[2]) + ((long long)row * W1 + w1) * a.ld[2] + col;
+                uint16_t *d = reinterpret_cast<uint16_t *>(a.lvl[2]) +
+                              ((long long)((MODE & kModeL2Stores) ? (row & 7) : row) * W1 + w1) * a.ld[2] + col;
                 const uint2 x = uint2{pack_bf16x2(qv[0], qv[1]), pack_bf16x2(qv[2], qv[3])};
                 *reinterpret_cast<uint2 *>(d) = x;
                 if (a.shadow[2]) *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(d) + a.shadow[2]) = x;
@@ -857,7 +858,8 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
                     uint2{h0[ma][nb][0], h0[ma][nb][1]};
         }
         uint16_t *l0 = reinterpret_cast<uint16_t *>(a.lvl[0]);
-        const long long rowbase = (long long)hrow * W1;
+        // kModeL2Stores (dev timing only, wrong output): 8 L2-resident rows
+        const long long rowbase = (long long)((MODE & kModeL2Stores) ? (hrow & 7) : hrow) * W1;
         for (int half = h0b; half < h1b; ++half) {
             const int R = 8 * half + (ln >> 3), c = ln & 7;
             const uint4 x = *reinterpret_cast<const uint4 *>(img + R * 144 + 16 * c);
@@ -1236,7 +1238,7 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
         else rc::launch_bf16_ring_two<0>(a, sh.defer, mode == 49 ? 2 : 1, s);
         return hipGetLastError();
     }
-    if (sh.nwn && mode >= 40 && mode <= 48) {
+    if (sh.nwn && mode >= 40 && mode <= 55 && mode != 49 && mode != 50 && mode != 51 && mode != 52 && mode != 53) {
         if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
         switch (mode) {
             case 40: rc::launch_bf16_ring<2>(a, sh, s); break;
@@ -1247,6 +1249,8 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
             case 43: rc::launch_bf16_ring<19>(a, sh, s); break;   // ... and no DMA
             case 46: rc::launch_bf16_ring<1>(a, sh, s); break;   // no DMA, with stores
             case 47: rc::launch_bf16_ring<5>(a, sh, s); break;   // no DMA, no MFMA, with stores
+            case 54: rc::launch_bf16_ring<rc::kModeL2Stores | 5>(a, sh, s); break;   // 47 with L2-resident stores
+            case 55: rc::launch_bf16_ring<rc::kModeL2Stores>(a, sh, s); break;       // product, L2-resident stores
             default: rc::launch_bf16_ring<10>(a, sh, s); break;
         }
         return hipGetLastError();
