@@ -167,11 +167,12 @@ __device__ __forceinline__ void flush_rows16_fast(uint32_t st, const BuildArgs &
         else if constexpr (VW == 2) asm volatile("ds_read_b64 %0, %1" : "=v"(x[k]) : "v"(src));
         else asm volatile("ds_read_b32 %0, %1" : "=v"(x[k]) : "v"(src));
     }
-    // the wait names the read registers, so no use of them moves above it
-    static_assert(NI == 1 || NI == 2 || NI == 4, "flush instruction count");
-    if constexpr (NI == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0])::"memory");
-    else if constexpr (NI == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0]), "+v"(x[1])::"memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3])::"memory");
+    // one wait, then the read registers pass through an asm each that
+    // follows it (volatile asms keep their order), so no use of them moves
+    // above the wait
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < NI; ++k) asm volatile("" : "+v"(x[k]));
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const int R = k * RPI + Rl, w1 = w1_0 + R;

@@ -101,7 +101,8 @@ __device__ __forceinline__ void split8_body(const Sp8Ctx &c, const BuildArgs &a,
     asm volatile("" ::: "memory");
     if constexpr (FA > 0) {
         const int m0 = c.M0 + c.img1 * c.ho1 + c.o1, n0 = c.N0 + c.img2 * c.ho2 + c.o2;
-        epilogue_swapped<FA, MODE, NLM>(acc, a, row, m0, n0, lane, lds_u32(smem + c.wave * kS8Stb), m0 + 16 * FB);
+        epilogue_swapped<FA, (MODE & kModeGenericEpi) ? MODE : (MODE | kModeFastEpi), NLM>(
+            acc, a, row, m0, n0, lane, lds_u32(smem + c.wave * kS8Stb), m0 + 16 * FB);
     }
 }
 
