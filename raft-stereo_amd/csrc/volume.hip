@@ -795,37 +795,50 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
         hrow = row; hm0 = m0h; hn0 = n0h; hact = act; held = true;
         if (!act) return;
         float s2[FMA][4];
+        // the scale as one wave-uniform branch around the whole block (a
+        // select per element would run the division sequence every time);
+        // each pair is rounded once: the packed bf16 is the level-0 value and
+        // its halves, widened, the pooling inputs (RNE is idempotent, so this
+        // equals rounding, widening and packing again)
+        auto level0 = [&](auto scale_fn) {
 #pragma unroll
-        for (int ma = 0; ma < FMA; ++ma)
+            for (int ma = 0; ma < FMA; ++ma)
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb) {
-                float vv[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float x = acc[ma][nb][r];
-                    vv[r] = round_bf16(a.pow2 ? x * a.scale : x / a.sq);
+                for (int nb = 0; nb < 4; ++nb) {
+                    const f32x4 x = acc[ma][nb];
+                    const uint32_t p0 = pack_bf16x2(scale_fn(x[0]), scale_fn(x[1]));
+                    const uint32_t p1 = pack_bf16x2(scale_fn(x[2]), scale_fn(x[3]));
+                    h0[ma][nb][0] = p0;
+                    h0[ma][nb][1] = p1;
+                    if constexpr ((MODE & kModeNoStores) != 0)   // dev timing: keep the MFMAs alive
+                        asm volatile("" ::"v"(p0), "v"(p1));
+                    const float v0 = __builtin_bit_cast(float, p0 << 16), v1 = __builtin_bit_cast(float, p0 & 0xFFFF0000u);
+                    const float v2 = __builtin_bit_cast(float, p1 << 16), v3 = __builtin_bit_cast(float, p1 & 0xFFFF0000u);
+                    s2[ma][nb] = pool2(pool2(v0, v1, true), pool2(v2, v3, true), true);
                 }
-                h0[ma][nb][0] = pack_bf16x2(vv[0], vv[1]);
-                h0[ma][nb][1] = pack_bf16x2(vv[2], vv[3]);
-                if constexpr ((MODE & kModeNoStores) != 0)       // dev timing: keep the MFMAs alive
-                    asm volatile("" ::"v"(h0[ma][nb][0]), "v"(h0[ma][nb][1]));
-                s2[ma][nb] = pool2(pool2(vv[0], vv[1], true), pool2(vv[2], vv[3], true), true);
-            }
+        };
+        if (a.pow2) {
+            const float sc = a.scale;
+            level0([sc](float x) { return x * sc; });
+        } else {
+            const float sq = a.sq;
+            level0([sq](float x) { return x / sq; });
+        }
+        // (hold runs for DEFER kernels only, which have FMA == 4)
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) {
-            float qv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                // source side: this lane offers its s2 of fragment (g - r) & 3;
-                // it receives from lane group (g + r) & 3 that group's value
-                // of fragment g
-                const int ms = (g - r) & 3;
-                const float x = ms == 0 ? s2[0][nb] : ms == 1 ? s2[1][nb] : ms == 2 ? s2[2][nb] : s2[3][nb];
-                const int src = (g + r) & 3;
-                const float y = r ? __shfl(x, i16 + 16 * src) : x;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) qv[j] = src == j ? y : qv[j];
-            }
+            // lane group g gets fragment g's level-2 value of every group j
+            // (a 4 x 4 transpose of 16-lane rows x fragments): two 32-lane
+            // swaps, then two 16-lane swaps -- afterwards register j of
+            // group g holds what group j had in register g
+            uint32_t R0 = __builtin_bit_cast(uint32_t, s2[0][nb]), R1 = __builtin_bit_cast(uint32_t, s2[1][nb]);
+            uint32_t R2 = __builtin_bit_cast(uint32_t, s2[2][nb]), R3 = __builtin_bit_cast(uint32_t, s2[3][nb]);
+            auto t02 = __builtin_amdgcn_permlane32_swap(R0, R2, false, false);
+            auto t13 = __builtin_amdgcn_permlane32_swap(R1, R3, false, false);
+            auto t01 = __builtin_amdgcn_permlane16_swap(t02[0], t13[0], false, false);
+            auto t23 = __builtin_amdgcn_permlane16_swap(t02[1], t13[1], false, false);
+            const float qv[4] = {__builtin_bit_cast(float, (uint32_t)t01[0]), __builtin_bit_cast(float, (uint32_t)t01[1]),
+                                 __builtin_bit_cast(float, (uint32_t)t23[0]), __builtin_bit_cast(float, (uint32_t)t23[1])};
             // level 2 is small (8 B per lane and column): stored right away
             const int w1 = m0h + 16 * nb + i16, col = (n0h >> 2) + 4 * g;
             if (!(MODE & kModeNoStores) && w1 < W1 && col < (W2 >> 2)) {
