@@ -558,16 +558,16 @@ __device__ __forceinline__ void fold_load(const BuildBwdArgs &a, long long prow,
 template <int NLEV>
 __device__ __forceinline__ f32x4 fold_math(const BuildBwdArgs &a, int w2, const FoldRaw<NLEV> &r) {
     constexpr int NC = FoldRaw<NLEV>::NC;
-    f32x4 out;
+    float d[4];
     if constexpr (NLEV == kPairFold) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const float t = (((w2 + c) >> 2) < a.Wl[2]) ? (r.lc[0] * 0.5f) * 0.5f : 0.0f;
             float d0 = r.g0[c] + t;
-            d0 = (w2 + c < a.W2) ? d0 : 0.0f;
-            out[c] = a.pow2 ? d0 * a.scale : d0 / a.sq;
+            d[c] = (w2 + c < a.W2) ? d0 : 0.0f;
         }
-        return out;
+        apply_scale(d, a);
+        return f32x4{d[0], d[1], d[2], d[3]};
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -578,10 +578,10 @@ __device__ __forceinline__ f32x4 fold_math(const BuildBwdArgs &a, int w2, const 
         if (NLEV >= 2 || (NLEV == 0 && a.nlev > 1))
             t = (((w2 + c) >> 1) < a.Wl[1]) ? r.l1[c >> 1] + t * 0.5f : 0.0f;
         float d0 = r.g0[c] + t * 0.5f;
-        d0 = (w2 + c < a.W2) ? d0 : 0.0f;   // the row padding may hold anything
-        out[c] = a.pow2 ? d0 * a.scale : d0 / a.sq;
+        d[c] = (w2 + c < a.W2) ? d0 : 0.0f;   // the row padding may hold anything
     }
-    return out;
+    apply_scale(d, a);
+    return f32x4{d[0], d[1], d[2], d[3]};
 }
 
 template <bool VEC>

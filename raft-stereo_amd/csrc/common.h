@@ -87,6 +87,23 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 // fp32 value rounded to bf16 precision (RNE), kept in fp32.
 __device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
 
+// v / sqrt(D) as the reference's division (model.py:326): a multiply by the
+// exact 1/sqrt(D) when D is a power of four (a.pow2), the correctly rounded
+// division otherwise.  One wave-uniform branch around the whole group: the
+// empty volatile asm keeps the division path a real branch, so the
+// power-of-two path never evaluates it (a select per element would).
+template <int N, class Args>
+__device__ __forceinline__ void apply_scale(float (&v)[N], const Args &a) {
+    if (a.pow2) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] *= a.scale;
+    } else {
+        asm volatile("");
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = v[k] / a.sq;
+    }
+}
+
 // Kernel parameter blocks (passed by value).
 struct BuildArgs {
     const void *f1, *f2;      // [B][D][H][W1], [B][D][H][W2]

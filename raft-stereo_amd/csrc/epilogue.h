@@ -468,11 +468,11 @@ __device__ __forceinline__ void epilogue_swapped(f32x4 (&acc)[FMA][4], const Bui
 #pragma unroll
         for (int ma = 0; ma < FMA; ++ma) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float x = acc[ma][0][r];
-                const float c = a.pow2 ? x * a.scale : x / a.sq;
-                v[ma][r] = bf ? round_bf16(c) : c;
-            }
+            for (int r = 0; r < 4; ++r) v[ma][r] = acc[ma][0][r];
+            apply_scale(v[ma], a);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (bf) v[ma][r] = round_bf16(v[ma][r]);
             acc[ma][0] = acc[ma][1];
             acc[ma][1] = acc[ma][2];
             acc[ma][2] = acc[ma][3];

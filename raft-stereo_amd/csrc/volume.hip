@@ -183,15 +183,15 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[FM][4], const BuildA
             const long long p = rowbase + w1;
             float c[4];
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb) {
-                const float v = acc[ma][nb][r];
-                c[nb] = a.pow2 ? v * a.scale : v / a.sq;
-                // a bf16 pyramid pools each level from the level below AS
-                // STORED (bf16), like avg_pool2d on a bf16 tensor and like
-                // rc_corr_pool: the pool-chain lookups can then derive a
-                // level from a stored one bit for bit
+            for (int nb = 0; nb < 4; ++nb) c[nb] = acc[ma][nb][r];
+            apply_scale(c, a);
+            // a bf16 pyramid pools each level from the level below AS
+            // STORED (bf16), like avg_pool2d on a bf16 tensor and like
+            // rc_corr_pool: the pool-chain lookups can then derive a level
+            // from a stored one bit for bit
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
                 if (bf) c[nb] = round_bf16(c[nb]);
-            }
             if constexpr (MODE & kModeNoStores) {
                 float keep = c[0] + c[1] + c[2] + c[3];
                 asm volatile("" ::"v"(keep));
