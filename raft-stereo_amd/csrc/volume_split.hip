@@ -52,6 +52,12 @@ struct SpCtx {
     int D, H, h, W1, W2, M0, N0, wave, lane, nst;
     int tw1, tw2;      // tile extent (w) along w1 / w2: 16 x fragments, <= 128
     int o1, o2;        // this wave's first column (w) inside the tile, w1 / w2
+    // DMA source offsets of this lane's two rows at stage 0 (F1, F2) and the
+    // per-stage step (kSpBK rows of d): a stage's offsets are one add away,
+    // no per-stage 32-bit multiplies (8 % of the K loop's VALU issue)
+    uint32_t oA[2], oB[2], sA, sB;
+    int dr0;           // this lane's d row inside a stage, first instruction
+    bool wA, wB;       // the lane's 4 columns inside the tile extent
 };
 
 // DMA share of this wave per stage: rows 4w..4w+3 of both tiles, 2 rows
@@ -63,12 +69,17 @@ __device__ __forceinline__ void sp_issue(const SpCtx &c, char *smem, int st) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r0 = 4 * c.wave + 2 * i;
-        const int d = st * kSpBK + r0 + (c.lane >> 5);
-        const int w = 4 * (c.lane & 31);
-        const long long base = (long long)(d < c.D ? d : 0) * c.H + c.h;
-        // columns past the tile extent are not fetched (out-of-range offset)
-        const uint32_t offA = d < c.D && w < c.tw1 ? (uint32_t)((base * c.W1 + c.M0 + w) * 4) : 0xFFFFFF00u;
-        const uint32_t offB = d < c.D && w < c.tw2 ? (uint32_t)((base * c.W2 + c.N0 + w) * 4) : 0xFFFFFF00u;
+        const int d = st * kSpBK + c.dr0 + 2 * i;
+        // rows d >= D and columns past the tile extent are not fetched
+        // (out-of-range offset)
+        uint32_t offA = d < c.D && c.wA ? c.oA[i] + (uint32_t)st * c.sA : 0xFFFFFF00u;
+        uint32_t offB = d < c.D && c.wB ? c.oB[i] + (uint32_t)st * c.sB : 0xFFFFFF00u;
+        if constexpr ((MODE & kModeOldAddr) != 0) {   // dev A/B: the per-stage multiplies of round 3
+            const int w = 4 * (c.lane & 31);
+            const long long base = (long long)(d < c.D ? d : 0) * c.H + c.h;
+            offA = d < c.D && w < c.tw1 ? (uint32_t)((base * c.W1 + c.M0 + w) * 4) : 0xFFFFFF00u;
+            offB = d < c.D && w < c.tw2 ? (uint32_t)((base * c.W2 + c.N0 + w) * 4) : 0xFFFFFF00u;
+        }
         if constexpr (!(MODE & kModeNoLoads)) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r1, (lds_void *)(sA + (r0 >> 1) * kSpBlk), 16, (int)offA, 0, 0, 0);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r2, (lds_void *)(sB + (r0 >> 1) * kSpBlk), 16, (int)offB, 0, 0, 0);
@@ -278,6 +289,20 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nw
     const int h1 = (tf1 + 1) >> 1, h2 = (tf2 + 1) >> 1;  // fragments of the first wave half
     c.o1 = 16 * h1 * wm; c.o2 = 16 * h2 * wn;
     c.nst = 2 * ((a.D + 2 * kSpBK - 1) / (2 * kSpBK));   // whole K steps (d >= D reads zeros)
+    {
+        const int w = 4 * (c.lane & 31);
+        c.dr0 = 4 * c.wave + (c.lane >> 5);
+        c.wA = w < c.tw1;
+        c.wB = w < c.tw2;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const long long base = (long long)(c.dr0 + 2 * i) * a.H + c.h;
+            c.oA[i] = (uint32_t)((base * a.W1 + c.M0 + w) * 4);
+            c.oB[i] = (uint32_t)((base * a.W2 + c.N0 + w) * 4);
+        }
+        c.sA = (uint32_t)kSpBK * (uint32_t)a.H * (uint32_t)a.W1 * 4u;
+        c.sB = (uint32_t)kSpBK * (uint32_t)a.H * (uint32_t)a.W2 * 4u;
+    }
     const long long img1 = (long long)a.D * a.H * a.W1, img2 = (long long)a.D * a.H * a.W2;
     c.r1 = make_rsrc(reinterpret_cast<const float *>(a.f1) + b * img1, clamp_bytes(img1 * 4));
     c.r2 = make_rsrc(reinterpret_cast<const float *>(a.f2) + b * img2, clamp_bytes(img2 * 4));
@@ -644,6 +669,7 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
         case 16384: hipLaunchKernelGGL((rc::build_split_kernel<16384, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 24576: hipLaunchKernelGGL((rc::build_split_kernel<24576, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 32768: hipLaunchKernelGGL((rc::build_split_kernel<32768, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
+        case 2097152: hipLaunchKernelGGL((rc::build_split_kernel<2097152, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 1048576: hipLaunchKernelGGL((rc::build_split_kernel<1048576, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 524288: hipLaunchKernelGGL((rc::build_split_kernel<524288, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
         case 524293: hipLaunchKernelGGL((rc::build_split_kernel<524288, rc::kSpMaxFused>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg, tf1, tf2, tiles1, tiles2); return hipGetLastError();
