@@ -789,6 +789,10 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
     // (g, i) the 4 level-2 values of fragment ma = g.
     uint32_t h0[FMA][4][2];
     int hrow = 0, hm0 = 0, hn0 = 0;
+    // per-lane row offsets of the deferred stores (elements): level-0 piece
+    // rows (lane >> 3) and 8 + (lane >> 3), level-2 row (lane & 15)
+    const int loff0 = (lane >> 3) * (int)a.ld[0], loff1 = loff0 + 8 * (int)a.ld[0];
+    const int l2off = (lane & 15) * (int)a.ld[2];
     bool hact = false, held = false;
     const int g = lane >> 4, i16 = lane & 15;
     auto hold = [&](int row, int m0h, int n0h, bool act) {
@@ -842,8 +846,8 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             // level 2 is small (8 B per lane and column): stored right away
             const int w1 = m0h + 16 * nb + i16, col = (n0h >> 2) + 4 * g;
             if (!(MODE & kModeNoStores) && w1 < W1 && col < (W2 >> 2)) {
-                uint16_t *d = reinterpret_cast<uint16_t *>(a.lvl[2]) +
-                              ((long long)((MODE & kModeL2Stores) ? (row & 7) : row) * W1 + w1) * a.ld[2] + col;
+                const long long r2 = (long long)((MODE & kModeL2Stores) ? (row & 7) : row) * W1 + m0h + 16 * nb;
+                uint16_t *d = reinterpret_cast<uint16_t *>(a.lvl[2]) + r2 * a.ld[2] + l2off + col;
                 const uint2 x = uint2{pack_bf16x2(qv[0], qv[1]), pack_bf16x2(qv[2], qv[3])};
                 *reinterpret_cast<uint2 *>(d) = x;
                 if (a.shadow[2]) *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(d) + a.shadow[2]) = x;
@@ -873,12 +877,15 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
         uint16_t *l0 = reinterpret_cast<uint16_t *>(a.lvl[0]);
         // kModeL2Stores (dev timing only, wrong output): 8 L2-resident rows
         const long long rowbase = (long long)((MODE & kModeL2Stores) ? (hrow & 7) : hrow) * W1;
+        // the piece's first row (wave-uniform, scalar math) + this lane's
+        // row offset (precomputed): no vector multiplies per store
+        uint16_t *t0 = l0 + (rowbase + hm0 + 16 * nb) * a.ld[0] + hn0;
         for (int half = h0b; half < h1b; ++half) {
             const int R = 8 * half + (ln >> 3), c = ln & 7;
             const uint4 x = *reinterpret_cast<const uint4 *>(img + R * 144 + 16 * c);
             const int w1 = hm0 + 16 * nb + R, col = hn0 + 8 * c;
             if (w1 < W1 && col < W2) {
-                uint16_t *d = l0 + (rowbase + w1) * a.ld[0] + col;
+                uint16_t *d = t0 + (half ? loff1 : loff0) + 8 * c;
                 *reinterpret_cast<uint4 *>(d) = x;
                 if (a.shadow[0]) *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(d) + a.shadow[0]) = x;
             }
