@@ -1,8 +1,10 @@
 """Benchmark of the RAFT-Stereo correlation path on MI355X.
 
 Contract (see task spec): ``python bench.py --gpus N --steps K --warmup W``;
-for N > 1 the driver launches one rank per GPU with torch.distributed.run.
-Rank 0 prints ONE JSON line.
+one rank per GPU.  Under a launcher (``torch.distributed.run``, WORLD_SIZE
+set) WORLD_SIZE must equal N; without one, ``--gpus N > 1`` starts the N
+ranks itself (a ``torch.distributed.run`` child, before this process touches
+the GPU).  Rank 0 prints ONE JSON line.
 
 Workload (BASELINE.json configs[1], the metric's config): SceneFlow-size
 540x960 stereo pairs, batch 8 per GPU, 32 GRU iterations, fp32 corr.  One
@@ -15,12 +17,18 @@ coords_grid - U[0, 64) per pixel, a fresh draw per iteration.
 
 value = stereo pairs/s through the corr path, all ranks (weak scaling: every
 rank processes its own batch of 8; the path shards by pair with no collective).
-The end-to-end model (encoders/GRU on PyTorch ops) is not in this number.
+The end-to-end model (encoders/GRU on PyTorch ops) is not in this number; it
+is reported beside it (``e2e``), and so is the row-sharded full network of
+BASELINE configs[3] (``config4_network``: 1984x2880, 32 iterations, GRU halo
+exchange over RCCL in the timed region).  ``--config middlebury --network``
+makes that network rate the line's ``value``.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -411,6 +419,91 @@ def pmc_entry(pmc, family):
     return hits[0] if len(hits) == 1 else (None, {})
 
 
+def launch_plan(gpus, env):
+    """How this invocation runs: ("run", world) -- this process is one rank
+    of ``world`` (WORLD_SIZE from a launcher, or 1) -- or ("spawn", gpus):
+    start ``gpus`` ranks under torch.distributed.run first.  A launcher whose
+    WORLD_SIZE disagrees with ``--gpus`` is an error (ValueError): the line
+    would otherwise report a world the caller did not ask for."""
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise ValueError(f"WORLD_SIZE={ws} from the launcher but --gpus {gpus}")
+        return "run", int(ws)
+    return ("spawn", gpus) if gpus > 1 else ("run", 1)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(gpus, argv, port):
+    """torch.distributed.run command for ``gpus`` ranks of this script on one
+    node (the driver's own form: 127.0.0.1 rendezvous, one rank per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def row_sharded_network(device, rank, world, steps, warmup, iters=32, image_hw=(1984, 2880)):
+    """BASELINE configs[3] end to end: ONE synthetic full-resolution pair,
+    RAFTStereo (seeded random-init weights, fp32, eval) row-sharded over the
+    ``world`` ranks by ``shard.RowShardedStereo`` -- encoders on each rank's
+    own rows with per-module halos and all-reduced InstanceNorm statistics,
+    the corr path on its rows, the GRU loop with its per-conv halo exchanges
+    (point-to-point; RCCL over xGMI when the group is nccl) -- 32 iterations.
+    Every exchange is inside the timed region.  Timed as the MAX over ranks
+    of the barrier-bracketed wall time (strong scaling: one pair per step)."""
+    from raft_stereo_amd.network import RAFTStereo, StereoArgs
+    from raft_stereo_amd.shard import RowShardedStereo
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs()).eval().to(device)
+    g = torch.Generator().manual_seed(1234)
+    H, W = image_hw
+    img1 = (torch.rand(1, 3, H, W, generator=g) * 255).to(device)
+    img2 = torch.roll(img1, shifts=-8, dims=-1)
+    rs = RowShardedStereo(model, rank, world)
+    with torch.no_grad():
+        for _ in range(warmup):
+            rs.forward(img1, img2, iters=iters)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        rs.xchg_wait_s, rs.xchg_count, rs.xchg_bytes, rs.xchg_posts = 0.0, 0, 0, 0
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            preds = rs.forward(img1, img2, iters=iters)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        own = time.perf_counter() - t0
+    dt = torch.tensor([own / steps], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    sec = float(dt.item())
+    hz = rs.perconv_halos()
+    r0, r1 = rs._own_rows(RowShardedStereo._heights(H, model.args.n_downsample,
+                                                    model.args.n_gru_layers), hz)
+    return {"pairs_per_s": 1.0 / sec, "ms_per_pair": sec * 1e3, "world": world,
+            "image": [H, W], "iters": iters, "steps": steps, "warmup": warmup,
+            "rank0_own_rows": [r0, r1], "halos": {k: hz[k] for k in ("net", "inp", "fmap", "coords")},
+            "rank0_exchanges_per_pair": rs.xchg_count / steps,
+            "rank0_recv_mb_per_pair": rs.xchg_bytes / steps / 1e6,
+            "rank0_wait_ms_per_pair": rs.xchg_wait_s / steps * 1e3,
+            "rank0_own_time_ms": own / steps * 1e3,
+            "flow_rows": int(preds[-1].shape[2]),
+            "backend": dist.get_backend() if world > 1 else None,
+            "note": "full network (encoders/GRU/heads on PyTorch ops, corr path on the HIP "
+                    "kernels), one 1984x2880 pair row-sharded over the ranks; halo exchanges "
+                    "and InstanceNorm all-reduces inside the timed region; max over ranks"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -442,13 +535,36 @@ def main():
                     help="skip the corr-path backward timing (sceneflow only)")
     ap.add_argument("--per-rank-of", type=int, default=0,
                     help="single-GPU projection input: run rank 0's share of an N-GPU job "
-                         "(kitti: batch 64/N; middlebury: H/N feature rows) and report the "
-                         "rate N such ranks would reach with no exchange (DESIGN.md §5)")
+                         "(kitti: batch 64/N; middlebury: H/N feature rows); value stays the "
+                         "measured work's rate, the N-rank rate goes to 'projection' (DESIGN.md §5)")
+    ap.add_argument("--shadow", default="default",
+                    help="pyramid levels with an RC_SHADOW copy: 'default' (per-shape rule, "
+                         "corr.default_shadow_levels), 'none', or a comma list such as 0,2")
+    ap.add_argument("--network", action="store_true",
+                    help="--config middlebury: the line's value is the row-sharded FULL network "
+                         "(BASELINE configs[3]: 1984x2880, 32 iterations, GRU halo exchange) "
+                         "instead of the corr path alone")
+    ap.add_argument("--config4-steps", type=int, default=1,
+                    help="default (sceneflow) run: also time the row-sharded config-4 network "
+                         "this many steps, after one warm-up (0 = skip)")
     args = ap.parse_args()
     if args.channels_last is None:   # NHWC output where it goes to HBM (the bf16 config)
         args.channels_last = args.config in BF16_CONFIGS
+    if args.network and args.config != "middlebury":
+        ap.error("--network applies to --config middlebury")
+    shadow = (None if args.shadow == "default" else () if args.shadow == "none"
+              else tuple(int(v) for v in args.shadow.split(",")))
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # one rank per GPU: decided before anything touches the GPU, so that the
+    # self-launch below starts its ranks from a process with no HIP context
+    try:
+        plan, world = launch_plan(args.gpus, os.environ)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        sys.exit(2)
+    if plan == "spawn":
+        cmd = launcher_cmd(world, sys.argv[1:], _free_port())
+        sys.exit(subprocess.run(cmd).returncode)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # RAFTCORR_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several
@@ -500,7 +616,8 @@ def main():
         if ev is not None:
             ev[0].record()
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
-                          low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
+                          low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32,
+                          shadow=shadow)
         if ev is not None:
             ev[1].record()
         for it in range(iters):
@@ -568,7 +685,8 @@ def main():
             torch.cuda._sleep(5_000_000)
             e0.record()
             CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
-                        low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
+                        low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32,
+                        shadow=shadow)
             e1.record()
             torch.cuda.synchronize()
             bl.append(e0.elapsed_time(e1))
@@ -580,7 +698,8 @@ def main():
         # GPU reaches them, so no event pair spans a host gap; median over 3
         # passes of all launches.
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
-                          low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32)
+                          low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32,
+                          shadow=shadow)
         per_launch = []
         for _ in range(3):
             le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
@@ -612,7 +731,14 @@ def main():
     # pairs the whole job processed per step: one row-sharded pair, the global
     # batch, or B per rank (weak scaling)
     job_pairs = 1 if row_shard else (CONFIGS[args.config][0] if global_batch else world * B)
-    value = job_pairs * args.steps / sec
+    if proj:
+        # one GPU ran only rank 0's share: value counts the work that ran (B
+        # pairs, or the row share of one pair); the N-rank rate is reported
+        # under "projection" only
+        run_pairs = (r1 - r0) / CONFIGS[args.config][2] if row_shard else B
+    else:
+        run_pairs = job_pairs
+    value = run_pairs * args.steps / sec
 
     vflops = volume_flops(B, D, H, W1, W2)
     s_el = 2 if bf16 else 4
@@ -690,13 +816,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if (row_shard or global_batch) else "weak",
+        "scaling": "strong" if ((row_shard or global_batch) and not proj) else "weak",
         "vs_baseline": None,
         "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (randn fmaps, coords_grid - U[0,64) per iteration)",
         "config": {"workload": desc + (" (HIP graph replay)" if args.graph else "")
                    + (f" (rows sharded over {world} ranks)" if row_shard else ""),
-                   "config": args.config, "global_batch": job_pairs,
+                   "config": args.config, "global_batch": run_pairs,
                    "fmap": [B, D, H, W1], "W2": W2, "levels": L, "radius": r, "iters": iters,
                    "parallelism": (f"row-shard x{world}" if row_shard else f"batch-shard x{world}"),
                    "corr_out_layout": "channels_last" if args.channels_last else "nchw"},
@@ -757,8 +883,33 @@ def main():
             "per_rank_of": proj, "rank_share": ({"rows": [r0, r1]} if row_shard else {"batch": B}),
             "projected_ms_per_step": ms_per_step,
             "projected_value": job_pairs / (ms_per_step * 1e-3),
-            "note": "single GPU timing rank 0's share; no collective in the timed path"}
+            "projected_global_batch": job_pairs,
+            "note": "single GPU timing rank 0's share; no collective in the timed path; "
+                    "projected_value assumes every rank takes as long -- not a measurement "
+                    "of N GPUs (the line's value is the work that ran, per second)"}
         result["config"]["parallelism"] = f"rank 0 of {proj} (single-GPU projection input)"
+    # BASELINE configs[3] end to end: in the default run as a side leg (so an
+    # N-GPU run of the default command measures config 4's scaling too), or as
+    # the line's value with --config middlebury --network
+    net_steps = (max(args.steps, 1) if args.network else
+                 args.config4_steps if args.config == "sceneflow" and not proj else 0)
+    if net_steps > 0:
+        leg = row_sharded_network(device, rank, world, net_steps, 1 if not args.network
+                                  else max(args.warmup, 1))
+        if args.network:
+            result["corr_path"] = {k: result[k] for k in ("value", "ms_per_step", "config")}
+            result.update({
+                "value": leg["pairs_per_s"], "ms_per_step": leg["ms_per_pair"],
+                "steps": net_steps, "warmup": leg["warmup"], "scaling": "strong",
+                "network": leg,
+                "config": {"workload": "BASELINE configs[3]: full RAFTStereo network, one "
+                                       "1984x2880 pair, 32 iterations, fp32, image rows sharded "
+                                       f"over {world} rank(s) (encoders with per-module halos, "
+                                       "corr path on own rows, GRU per-conv halo exchange)",
+                           "config": "middlebury", "global_batch": 1, "image": [1984, 2880],
+                           "iters": 32, "parallelism": f"row-shard x{world}"}})
+        else:
+            result["config4_network"] = leg
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds,
                                               full=args.config == "sceneflow")

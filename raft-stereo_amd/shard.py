@@ -17,6 +17,7 @@ import time
 
 import torch
 import torch.distributed as dist
+import torch.nn.functional as F
 
 from .corr import CorrBlock1D, coords_grid
 
@@ -107,6 +108,136 @@ def _interp_rows(x, src_lo, src_glob, dst_lo, dst_hi, dst_glob, dst_w):
                                            align_corners=True)
 
 
+class _Rows:
+    """Rows [g0, g0 + t.shape[2]) of a feature level of global height H
+    (held rows outside [0, H), if any, are zeros)."""
+    __slots__ = ("t", "g0", "H")
+
+    def __init__(self, t, g0, H):
+        self.t, self.g0, self.H = t, g0, H
+
+    @property
+    def g1(self):
+        return self.g0 + self.t.shape[2]
+
+    def clip(self, lo, hi):
+        """[lo, hi) cut to the image; raises if a row inside it is not held
+        (a halo too small for the op that asked)."""
+        s0, s1 = max(lo, 0), min(hi, self.H)
+        if s0 < max(self.g0, 0) or s1 > min(self.g1, self.H):
+            raise RuntimeError(f"rows [{lo}, {hi}) of a level of {self.H} rows requested from "
+                               f"the held rows [{self.g0}, {self.g1})")
+        return s0, s1
+
+    def rows(self, lo, hi):
+        """Global rows [lo, hi); rows outside [0, H) are zeros -- the zero
+        padding the full-image op applies there (a view when held)."""
+        if self.g0 <= lo and hi <= self.g1:
+            return self.t[:, :, lo - self.g0:hi - self.g0]
+        s0, s1 = self.clip(lo, hi)
+        return F.pad(self.t[:, :, s0 - self.g0:s1 - self.g0], (0, 0, s0 - lo, hi - s1))
+
+
+def _conv_rows(conv, x, lo, hi):
+    """``conv`` (stride 1, zero 'same' padding) evaluated on output rows
+    [lo, hi) only, clipped to the level: the full-image op's values on those
+    rows.  It reads the held input rows [lo - p, hi + p) with no row padding;
+    where that range leaves the image, the conv's own zero padding supplies
+    the missing rows (the extra output rows of an asymmetric edge are cut)."""
+    lo, hi = max(lo, 0), min(hi, x.H)
+    p, pw = conv.padding
+    if x.g0 <= lo - p and hi + p <= x.g1:
+        y = F.conv2d(x.rows(lo - p, hi + p), conv.weight, conv.bias, conv.stride, (0, pw),
+                     conv.dilation, conv.groups)
+    else:
+        s0, s1 = x.clip(lo - p, hi + p)
+        m = max(s0 - (lo - p), (hi + p) - s1)          # zero rows the image edge supplies
+        y = F.conv2d(x.t[:, :, s0 - x.g0:s1 - x.g0], conv.weight, conv.bias, conv.stride, (m, pw),
+                     conv.dilation, conv.groups)
+        k0 = lo - s0 + m - p
+        if k0 or y.shape[2] != hi - lo:
+            y = y[:, :, k0:k0 + hi - lo]
+    return _Rows(y, lo, x.H)
+
+
+def _pool_rows(x, lo, hi, H):
+    """pool2x (model.py:182-183: 3x3, stride 2, zero padding counted) of the
+    level held by ``x`` on output rows [lo, hi) of the pooled level (height
+    ``H``): input rows [2lo-1, 2hi), the image's zero rows supplied by the
+    pool's own padding where the stride grid allows, else explicitly -- every
+    window is 3 full rows, as in the full op."""
+    lo, hi = max(lo, 0), min(hi, H)
+    a, b = 2 * lo - 1, 2 * hi
+    if x.g0 <= a and b <= x.g1:
+        y = F.avg_pool2d(x.rows(a, b), 3, stride=2, padding=(0, 1))
+    else:
+        s0, s1 = x.clip(a, b)
+        if s0 - a == 1:            # the top image edge: the pool's padding row, grid aligned
+            y = F.avg_pool2d(x.t[:, :, s0 - x.g0:s1 - x.g0], 3, stride=2, padding=1)
+            if y.shape[2] != hi - lo:
+                y = y[:, :, :hi - lo]
+        else:
+            y = F.avg_pool2d(x.rows(a, b), 3, stride=2, padding=(0, 1))
+    return _Rows(y, lo, H)
+
+
+def _interp_rows_held(x, lo, hi, H, W):
+    """interp (model.py:184-186: bilinear, align_corners=True) of the level
+    held by ``x`` to a level of H x W, on destination rows [lo, hi) only; the
+    source rows the global row mapping reads must be held."""
+    lo, hi = max(lo, 0), min(hi, H)
+    scale = (x.H - 1) / (H - 1) if H > 1 else 0.0
+    # the source rows _interp_rows reads, in its own fp32 arithmetic
+    ends = (torch.tensor([lo, hi - 1], dtype=torch.float32) * scale).clamp(max=x.H - 1).floor()
+    need0, need1 = int(ends[0]), min(int(ends[1]) + 2, x.H)
+    if need0 < x.g0 or need1 > x.g1:
+        raise RuntimeError(f"interp rows [{lo}, {hi}) need source rows [{need0}, {need1}) of "
+                           f"the held [{x.g0}, {x.g1})")
+    return _Rows(_interp_rows(x.t, x.g0, x.H, lo, hi, H, W), lo, H)
+
+
+def _relu(x):
+    return _Rows(F.relu(x.t), x.g0, x.H)
+
+
+def _cat_rows(parts, lo, hi):
+    """Channel concatenation of several _Rows on rows [lo, hi) cut to the
+    image (one copy, as the full op's torch.cat)."""
+    s0, s1 = parts[0].clip(lo, hi)
+    return _Rows(torch.cat([p.rows(s0, s1) for p in parts], 1), s0, parts[0].H)
+
+
+def _gru_rows(gru, h, cz, cr, cq, xs, lo, hi):
+    """ConvGRU.forward (model.py:164-179) on output rows [lo, hi): z on
+    [lo, hi), r on the rows convq reads, both from [h, x] on one more cone
+    of rows; r*h and x zero outside the image as the full op pads them.
+    ``h``, ``cz``, ``cr``, ``cq`` and each of ``xs`` are _Rows holding
+    enough rows.  Returns the new hidden state's rows [lo, hi)."""
+    H = h.H
+    p, pq = gru.convz.padding[0], gru.convq.padding[0]
+    ra, rb = max(lo - pq, 0), min(hi + pq, H)                 # rows of r (convq's input)
+    hx = _cat_rows([h] + list(xs), ra - p, rb + p)
+    z = torch.sigmoid(_conv_rows(gru.convz, hx, lo, hi).t + cz.rows(lo, hi))
+    r = torch.sigmoid(_conv_rows(gru.convr, hx, ra, rb).t + cr.rows(ra, rb))
+    rx = _cat_rows([_Rows(r * h.rows(ra, rb), ra, H)] + list(xs), ra, rb)
+    q = torch.tanh(_conv_rows(gru.convq, rx, lo, hi).t + cq.rows(lo, hi))
+    return (1 - z) * h.rows(lo, hi) + z * q
+
+
+def _motion_rows(enc, corr, flow, lo, hi):
+    """BasicMotionEncoder.forward (model.py:192-213) on output rows [lo, hi)
+    from ``corr`` and ``flow`` _Rows holding the rows its cone reads."""
+    k = enc.conv.padding[0]
+    c = _relu(_conv_rows(enc.convc1, corr, lo - k - enc.convc2.padding[0],
+                         hi + k + enc.convc2.padding[0]))
+    c = _relu(_conv_rows(enc.convc2, c, lo - k, hi + k))
+    f = _relu(_conv_rows(enc.convf1, flow, lo - k - enc.convf2.padding[0],
+                         hi + k + enc.convf2.padding[0]))
+    f = _relu(_conv_rows(enc.convf2, f, lo - k, hi + k))
+    out = _relu(_conv_rows(enc.conv, _cat_rows([c, f], lo - k, hi + k), lo, hi))
+    return _cat_rows([out, flow], out.g0, out.g1)
+
+
 def _all_reduce_sum(t, group=None):
     """In-place SUM all-reduce (host-staged for gloo on CUDA tensors)."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
@@ -176,7 +307,13 @@ class RowShardedStereo:
     """
 
     def __init__(self, model, rank, world, halo=None, group=None, shard_encoders=True, enc_margin=48,
-                 per_stage=True, encoder_halos=True, overlap=True):
+                 per_stage=True, encoder_halos=True, overlap=True, per_conv=None):
+        # per_conv (the default unless a slab ``halo`` or per_stage=False is
+        # asked for): GRU state on own rows, each conv evaluated on the rows its
+        # readers need, halos exchanged per update (_forward_perconv)
+        if per_conv is None:
+            per_conv = halo is None and per_stage
+        self.per_conv = bool(per_conv)
         # one stage's cone needs 12 rows; a whole iteration's up to 20
         if halo is None:
             halo = 12 if per_stage else 24
@@ -206,6 +343,9 @@ class RowShardedStereo:
         self._fake_xchg = False     # tools/shard_probe.py: time one rank's compute alone
         self.xchg_wait_s = 0.0      # host time spent blocked in exchange waits
         self.xchg_count = 0
+        self.xchg_posts = 0         # halo exchanges posted (_halo_start)
+        self.xchg_bytes = 0         # bytes received by them
+        self.xchg_link_bytes = 0    # the larger neighbour's share of each
 
     # row geometry -----------------------------------------------------------
     def _ranges(self, H1):
@@ -342,6 +482,13 @@ class RowShardedStereo:
         g0, g1 = max(0, lo - h), min(Hg, hi + h)
         if self.world == 1 or h == 0:
             return ("done", t, lo)
+        # message accounting (tools/shard_probe.py): rows received from each
+        # neighbour; the two links run concurrently, so the larger side is the
+        # exchange's per-link transfer
+        row = t[:, :, :1].numel() * t.element_size()
+        self.xchg_posts += 1
+        self.xchg_bytes += (lo - g0 + g1 - hi) * row
+        self.xchg_link_bytes += max(lo - g0, g1 - hi) * row
         if self._fake_xchg:          # timing probe: same shapes, no communication
             top = t.new_zeros(t.shape[:2] + (lo - g0,) + t.shape[3:])
             bot = t.new_zeros(t.shape[:2] + (g1 - hi,) + t.shape[3:])
@@ -525,10 +672,207 @@ class RowShardedStereo:
             out_i.append(pieces[1:])
         return out_f[0], out_f[1], out_n, out_i
 
+    # per-conv halos (default) ---------------------------------------------
+    def perconv_halos(self):
+        """Rows of halo each GRU-loop tensor needs at its own level, from the
+        receptive fields of the ops that read it (model.py:164-265):
+          gp  = one ConvGRU's cone (convz/convr, then convq on r*h): 2 rows;
+          net[l]: its own GRU (gp), the next coarser GRU's pool2x input
+                  (2*gp + 1 = 5), the finer GRU's interp (<= gp), level 0
+                  also the flow head (conv1 + conv2: 2);
+          inp (context biases): convr's rows of r (1);
+          fmaps: gru08's cone + the motion encoder's corr branch (1x1, 3x3,
+                 3x3): 4 -- the corr block is built on own rows +- 4;
+          coords1: gru08's cone + the flow branch (7x7, 3x3, 3x3): 7."""
+        blk, n = self.model.update_block, self.model.args.n_gru_layers
+        grus = [blk.gru08, blk.gru16, blk.gru32][:n]
+        gp = [g.convz.padding[0] + g.convq.padding[0] for g in grus]
+        enc, fh = blk.encoder, blk.flow_head
+        k = enc.conv.padding[0]
+        net = []
+        for l in range(n):
+            need = gp[l]
+            if l == 0:
+                need = max(need, fh.conv1.padding[0] + fh.conv2.padding[0])
+            if l + 1 < n:
+                need = max(need, 2 * gp[l + 1] + 1)
+            if l > 0:
+                need = max(need, gp[l - 1])
+            net.append(need)
+        return {"net": net, "inp": max(g.convq.padding[0] for g in grus),
+                "fmap": gp[0] + k + enc.convc2.padding[0] + enc.convc1.padding[0],
+                "coords": gp[0] + k + enc.convf2.padding[0] + enc.convf1.padding[0],
+                "gp": gp}
+
+    def _own_rows(self, glob, hz):
+        """This rank's 1/4-res rows [r0, r1) (multiples of 4); every rank but
+        the last must own at least the halo rows each level exchanges (a halo
+        comes from the direct neighbour only)."""
+        H1 = glob[0]
+        nblk = (H1 + 3) // 4
+        need = [max([hz["net"][l], hz["inp"]] + ([hz["coords"], hz["fmap"]] if l == 0 else []))
+                for l in range(len(glob))]
+        for k in range(self.world - 1):
+            b0, b1 = split_range(nblk, k, self.world)
+            for l, h in enumerate(need):
+                lo, hi = self._lvl(4 * b0, min(4 * b1, H1), l)
+                if hi - lo < h:
+                    raise ValueError(f"rank {k} owns {hi - lo} rows at level {l} < the {h}-row "
+                                     "halo: use fewer ranks")
+        b0, b1 = split_range(nblk, self.rank, self.world)
+        return 4 * b0, min(4 * b1, H1)
+
+    def _perconv_state(self, image1, image2, r0, r1, glob, hz):
+        """Encoders -> _Rows of fmap1, fmap2 (own rows +- the fmap halo),
+        every level's net (own rows + its halo) and context biases (+- 1)."""
+        m, n = self.model, self.model.args.n_gru_layers
+        if self.shard_encoders and not m.training and self.encoder_halos:
+            f1, f2, net, inp, levels, _ = self._features_halo(image1, image2, r0, r1)
+            fS, netS, inpS = None, [], []
+            for l, (lo, hi, Hg) in enumerate(levels):
+                parts = ([f1, f2] if l == 0 else []) + [net[l]] + inp[l]
+                h = max([hz["net"][l], hz["inp"]] + ([hz["fmap"]] if l == 0 else []))
+                dt = parts[0].dtype
+                for p in parts[1:]:
+                    dt = torch.promote_types(dt, p.dtype)
+                slab, g0 = self._halo(torch.cat([p.to(dt) for p in parts], 1), lo, hi, Hg, h)
+                pieces = [pc.to(p.dtype) for pc, p in
+                          zip(slab.split([p.shape[1] for p in parts], 1), parts)]
+                if l == 0:
+                    fS = (_Rows(pieces[0], g0, Hg), _Rows(pieces[1], g0, Hg))
+                    pieces = pieces[2:]
+                netS.append(_Rows(pieces[0], g0, Hg))
+                inpS.append([_Rows(c, g0, Hg) for c in pieces[1:]])
+            return fS, netS, inpS
+        if self.shard_encoders and not m.training:
+            # round 2's band encoders: a slab of own rows +- 12 (covers every
+            # halo above at every level) with enc_margin recomputed rows
+            H1 = glob[0]
+            e0, e1 = max(0, r0 - 12), min(H1, r1 + 12)
+            f1, f2, net, inp = self._features_rows(image1, image2, e0, e1, r0, r1)
+            g = [self._lvl(e0, e1, l)[0] for l in range(n)]
+            return ((_Rows(f1, e0, H1), _Rows(f2, e0, H1)),
+                    [_Rows(net[l], g[l], glob[l]) for l in range(n)],
+                    [[_Rows(c, g[l], glob[l]) for c in inp[l]] for l in range(n)])
+        # replicated encoders (or train mode): the full image's features
+        f1, f2, net, inp = m.features(image1, image2)
+        return ((_Rows(f1, 0, glob[0]), _Rows(f2, 0, glob[0])),
+                [_Rows(net[l], 0, glob[l]) for l in range(n)],
+                [[_Rows(c, 0, glob[l]) for c in inp[l]] for l in range(n)])
+
+    def _forward_perconv(self, image1, image2, iters):
+        """The GRU loop with per-conv halos: every tensor lives on the rank's
+        OWN rows; each op is evaluated on exactly the rows its consumers read
+        (_conv_rows, _pool_rows, _interp_rows_held: the full-image op's values
+        there, zero padding at the image edges), and after each update the
+        new rows' halo (perconv_halos) is posted to the two neighbours and
+        waited for at its first reader:
+          gru32 -> post net[2] | wait coords1 (previous iteration); corr
+                               | lookup on own rows +- 4; flow; motion encoder
+          wait net[2] -> gru16 -> post net[1]
+          wait net[1] -> gru08 -> post net[0] -> wait -> flow head on own rows
+          coords1 update -> post coords1 | next iteration's gru32
+        Nothing is recomputed beyond the halo rows a conv's own receptive field
+        needs, so per-rank work is own rows + O(1) rows per conv (the slab of
+        the per-stage mode carried 12 extra rows on either side)."""
+        m, a = self.model, self.model.args
+        blk, n = m.update_block, a.n_gru_layers
+        glob = self._heights(image1.shape[2], a.n_downsample, n)
+        H1 = glob[0]
+        hz = self.perconv_halos()
+        r0, r1 = self._own_rows(glob, hz)
+        own = [self._lvl(r0, r1, l) for l in range(n)]
+        fS, netS, inpS = self._perconv_state(image1, image2, r0, r1, glob, hz)
+        c0, c1 = max(0, r0 - hz["fmap"]), min(H1, r1 + hz["fmap"])
+        corr_fn = m.corr_block(fS[0].rows(c0, c1).contiguous(), fS[1].rows(c0, c1).contiguous(),
+                               radius=a.corr_radius, num_levels=a.corr_levels)
+        del fS
+        B, W1 = netS[0].t.shape[0], netS[0].t.shape[3]
+        widths = [netS[l].t.shape[3] for l in range(n)]
+        grid = coords_grid(B, H1, W1).to(netS[0].t.device)
+        hc = hz["coords"]
+        k0, k1 = max(0, r0 - hc), min(H1, r1 + hc)
+        coords0 = grid[:, :, k0:k1]
+        state = {"net0": netS[0], "coords": _Rows(coords0.clone(), k0, H1)}
+        if n > 1:
+            state["net1"] = netS[1]
+        if n > 2:
+            state["net2"] = netS[2]
+        gp = hz["gp"]
+
+        def post(key, t, l, h):
+            hd = self._halo_start(t, own[l][0], own[l][1], glob[l], h)
+            state[key] = ("pending", hd, glob[l])
+            if not self.overlap:
+                get(key)
+
+        def get(key):
+            v = state[key]
+            if isinstance(v, tuple):
+                t, g0 = self._halo_finish(v[1])
+                v = state[key] = _Rows(t, g0, v[2])
+            return v
+
+        def gru(l, xs):
+            g = (blk.gru08, blk.gru16, blk.gru32)[l]
+            lo, hi = own[l]
+            h = _gru_rows(g, get(f"net{l}"), *inpS[l], xs, lo, hi)
+            post(f"net{l}", h, l, hz["net"][l])
+
+        def gru32():
+            lo, hi = own[2]
+            gru(2, [_pool_rows(get("net1"), lo - gp[2], hi + gp[2], glob[2])])
+
+        def gru16():
+            lo, hi = own[1]
+            xs = [_pool_rows(get("net0"), lo - gp[1], hi + gp[1], glob[1])]
+            if n == 3:
+                xs.append(_interp_rows_held(get("net2"), lo - gp[1], hi + gp[1], glob[1], widths[1]))
+            gru(1, xs)
+
+        preds = []
+        lo0, hi0 = own[0]
+        fh = blk.flow_head
+        p2 = fh.conv2.padding[0]
+        for _ in range(iters):
+            with m._autocast():
+                if n == 3 and a.slow_fast_gru:
+                    gru32()
+                if n >= 2 and a.slow_fast_gru:
+                    if n == 3:
+                        gru32()
+                    gru16()
+                if n == 3:
+                    gru32()
+            cS = get("coords")
+            corr = _Rows(corr_fn(cS.rows(c0, c1).contiguous()), c0, H1)
+            flow = _Rows(cS.t - coords0, k0, H1)
+            with m._autocast():
+                motion = _motion_rows(blk.encoder, corr, flow, lo0 - gp[0], hi0 + gp[0])
+                if n >= 2:
+                    gru16()
+                xs = [motion]
+                if n > 1:
+                    xs.append(_interp_rows_held(get("net1"), lo0 - gp[0], hi0 + gp[0], glob[0],
+                                                widths[0]))
+                gru(0, xs)
+                hid = _relu(_conv_rows(fh.conv1, get("net0"), lo0 - p2, hi0 + p2))
+                delta = _conv_rows(fh.conv2, hid, lo0, hi0).t
+            delta = delta.float()
+            delta[:, 1] = 0.0
+            c_own = cS.rows(lo0, hi0) + delta
+            preds.append(c_own - grid[:, :, lo0:hi0])
+            post("coords", c_own, 0, hc)
+        for key in list(state):         # drain the last iteration's exchanges
+            get(key)
+        return preds
+
     # forward ----------------------------------------------------------------
     def forward(self, image1, image2, iters=12):
         m, a = self.model, self.model.args
         nl = a.n_gru_layers
+        if self.per_conv:
+            return self._forward_perconv(image1, image2, iters)
         # train-mode BatchNorm needs the whole image's batch statistics: the
         # replicated encoders give exactly the unsharded network's features
         if self.shard_encoders and not m.training:

@@ -29,7 +29,7 @@ def row_case():
     return f1, f2, torch.cat([x, torch.zeros(2, 1, 7, 24)], 1)
 
 
-def model(slow_fast=False):
+def model(slow_fast=False, n_gru_layers=None):
     import torch
     import pkgload
     pkgload.load()
@@ -41,6 +41,8 @@ def model(slow_fast=False):
     args = dict(case["args"])
     if slow_fast:
         args["slow_fast_gru"] = True
+    if n_gru_layers is not None:
+        args["n_gru_layers"] = n_gru_layers
     return RAFTStereo(StereoArgs(**args), corr_block=torch_ref.TorchCorrBlock1D).eval()
 
 
@@ -74,8 +76,10 @@ def run(rank, world, port, q):
 
 
 def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders=True,
-             per_stage=False, overlap=True, slow_fast=False):
-    """Row-sharded network forward vs the unsharded one (oracle corr block)."""
+             per_stage=False, overlap=True, slow_fast=False, per_conv=None, encoder_halos=True,
+             n_gru_layers=None):
+    """Row-sharded network forward vs the unsharded one (oracle corr block);
+    ``halo=None`` with per_stage: the per-conv default."""
     import torch
     import torch.distributed as dist
     import pkgload
@@ -89,9 +93,10 @@ def run_rows(rank, world, port, q, halo=32, H=144, W=96, iters=4, shard_encoders
         g = torch.Generator().manual_seed(3)
         img1 = torch.rand(1, 3, H, W, generator=g) * 255
         img2 = torch.roll(img1, -4, dims=-1)
-        net = model(slow_fast=slow_fast)
+        net = model(slow_fast=slow_fast, n_gru_layers=n_gru_layers)
         rs = RowShardedStereo(net, rank, world, halo=halo, shard_encoders=shard_encoders,
-                              per_stage=per_stage, overlap=overlap)
+                              per_stage=per_stage, overlap=overlap, per_conv=per_conv,
+                              encoder_halos=encoder_halos)
         with torch.no_grad():
             preds = rs.forward(img1, img2, iters=iters)
             full = [rs.gather_rows(p) for p in preds]

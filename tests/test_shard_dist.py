@@ -154,3 +154,59 @@ def test_gloo_encoder_halo_exchange_matches_full(world, H, layers, down, f64):
     H1 = res[0][1][0]
     assert owns[0][0] == 0 and owns[-1][1] == H1
     assert all(a[1] == b[0] for a, b in zip(owns, owns[1:]))
+
+
+@pytest.mark.parametrize("world,H,W,shard_enc,enc_halos,slow_fast,layers", [
+    (2, 320, 96, True, True, False, 3), (3, 320, 96, True, True, False, 3),
+    (3, 320, 96, False, True, False, 3), (2, 320, 96, True, False, True, 3),
+    (3, 320, 96, True, True, True, 2), (2, 320, 64, True, True, False, 1)])
+def test_gloo_perconv_row_sharded_network(world, H, W, shard_enc, enc_halos, slow_fast, layers):
+    """the default row-sharded GRU loop keeps every tensor
+    on the rank's OWN rows and evaluates each conv / pool / interp on exactly
+    the rows its readers need, with the halos (2-7 rows per tensor at its own
+    level, RowShardedStereo.perconv_halos) exchanged after each update
+    (model.py:164-265) -- equal to the unsharded network to fp32 rounding
+    (CPU convolutions of other input heights pick other summation orders),
+    for the three encoder modes, the slow-fast schedule and 1-3 GRU levels."""
+    iters = 4
+    res = _spawn(dist_worker.run_rows, world, None, H, W, iters, shard_enc, True, True,
+                 slow_fast, True, enc_halos, layers)
+    g = torch.Generator().manual_seed(3)
+    img1 = torch.rand(1, 3, H, W, generator=g) * 255
+    img2 = torch.roll(img1, -4, dims=-1)
+    with torch.no_grad():
+        ref = torch.stack(dist_worker.model(slow_fast, layers)(img1, img2, iters=iters))
+    for r in range(world):
+        got = res[r][0]
+        assert got.shape == ref.shape
+        assert (got - ref).abs().max() < 5e-5, (got - ref).abs().max()
+        assert (got - ref).abs().mean() < 1e-6
+
+
+def test_gloo_perconv_overlap_equals_blocking():
+    """Per-conv mode: exchanges posted at the update and waited for at the
+    first reader give the same flows, bit for bit, as waiting right away."""
+    got = {}
+    for overlap in (True, False):
+        res = _spawn(dist_worker.run_rows, 3, None, 320, 96, 3, True, True, overlap, False, True)
+        got[overlap] = res[0][0]
+        for r in range(3):
+            assert torch.equal(res[r][0], got[overlap])
+    assert torch.equal(got[True], got[False])
+
+
+def test_perconv_halos_and_rank_limit():
+    """The halo table follows the modules' receptive fields, and a world so
+    large that a rank owns fewer rows than a halo is refused up front."""
+    from raft_stereo_amd.shard import RowShardedStereo
+    rs = RowShardedStereo(dist_worker.model(), 0, 1)
+    assert rs.per_conv
+    hz = rs.perconv_halos()
+    assert hz["net"] == [5, 5, 2] and hz["inp"] == 1 and hz["fmap"] == 4 and hz["coords"] == 7
+    glob = RowShardedStereo._heights(1984, 2, 3)
+    assert glob == [496, 248, 124]
+    for world in (1, 2, 4, 8):
+        r0, r1 = RowShardedStereo(dist_worker.model(), world - 1, world)._own_rows(glob, hz)
+        assert r1 == 496 and r0 % 4 == 0
+    with pytest.raises(ValueError, match="halo"):
+        RowShardedStereo(dist_worker.model(), 0, 62)._own_rows(glob, hz)

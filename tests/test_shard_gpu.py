@@ -35,23 +35,27 @@ def _reference():
     return net, batch, rows
 
 
-def test_world1_sharding_on_hip_path():
+@pytest.mark.parametrize("halo", [32, None])
+def test_world1_sharding_on_hip_path(halo):
+    """``halo=None``: the per-conv default (own rows, conv-sized halos)."""
     from raft_stereo_amd.shard import RowShardedStereo, gather_batch
     net, batch, rows = _reference()
     img1, img2 = dist_worker.pairs()
     r1, r2 = dist_worker.rows_images()
     with torch.no_grad():
         got = gather_batch(net(img1.cuda(), img2.cuda(), iters=3)[-1], 1).cpu()
-        rs = RowShardedStereo(net, 0, 1, halo=32)
+        rs = RowShardedStereo(net, 0, 1, halo=halo)
+        assert rs.per_conv == (halo is None)
         got_rows = torch.stack([rs.gather_rows(p) for p in rs.forward(r1.cuda(), r2.cuda(), iters=4)])
     assert (got - batch).abs().mean() <= MAE_PX
     assert got_rows.shape == rows.shape
     assert (got_rows.cpu() - rows).abs().mean() <= MAE_PX
 
 
-def test_world2_sharding_on_hip_path():
+@pytest.mark.parametrize("halo", [32, None])
+def test_world2_sharding_on_hip_path(halo):
     _, batch, rows = _reference()
-    res = _spawn(dist_worker.run_gpu, 2)
+    res = _spawn(dist_worker.run_gpu, 2, halo)
     for r in range(2):
         full, got_rows = res[r]
         assert full.shape == batch.shape

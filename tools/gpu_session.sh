@@ -115,6 +115,22 @@ if has proj; then   # per-rank shapes at N = 1/2/4/8 on one GPU (projection inpu
         step proj_middlebury_$N 300 python bench.py --config middlebury --per-rank-of $N --no-cpu-baseline --steps 5 --warmup 2
     done
 fi
+has shardt && step pytest_shard 600 python -u -m pytest tests/test_shard_gpu.py -v -rf --timeout 300 --timeout-method thread
+# bench.py --gpus 2 without a launcher (self-launch), 2 ranks sharing cuda:0 over gloo
+has launch && step launch_gloo2 600 env RAFTCORR_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 0 --no-backward
+has netmb && step net_middlebury_1 600 python bench.py --config middlebury --network --steps 2 --warmup 1 --no-cpu-baseline
+has netmb && step net_middlebury_gloo2 900 env RAFTCORR_BENCH_BACKEND=gloo python bench.py --gpus 2 --config middlebury --network --steps 1 --warmup 1 --no-cpu-baseline
+has pconv && step shard_probe_perconv 900 python tools/shard_probe.py --perconv
+if has shadowk; then   # config-3 shadow copies re-decided as whole steps
+    for rep in 1 2; do
+        for SH in default 2 none; do
+            step shadowk_b64_${SH}_$rep 300 python bench.py --config kitti --no-cpu-baseline --steps 10 --warmup 3 --shadow $SH
+        done
+        for SH in default 0,2 none; do
+            step shadowk_b8_${SH/,/}_$rep 300 python bench.py --config kitti --per-rank-of 8 --no-cpu-baseline --steps 20 --warmup 5 --shadow $SH
+        done
+    done
+fi
 has shard8 && step shard_probe_h8 900 python tools/shard_probe.py --halo 8
 has sabl && step build_ablate 600 python tools/build_ablate.py --modes ${SABL_MODES:-0,8192} --rounds ${SABL_ROUNDS:-9} ${SABL_CONFIG:+--config $SABL_CONFIG}
 has shear && step shear_probe 600 python tools/shear_probe.py

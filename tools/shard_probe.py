@@ -32,6 +32,18 @@ over gloo run RowShardedStereo.forward on a small image with the exchanges
 overlapped (the default) and blocking, and report per rank the forward time,
 the host time blocked in exchange waits (``xchg_wait_s``) and the number of
 waits.  A CPU/gloo rehearsal of the schedule, not an xGMI measurement.
+
+    python tools/shard_probe.py --perconv [--link-gbs 153 --msg-us 15]
+
+The default per-conv mode end to end: for N = 1, 2, 4, 8
+a middle rank's WHOLE RowShardedStereo.forward (encoders with per-module
+halos, corr build on own rows +- 4, 32 GRU iterations with per-conv halos)
+on one GPU, exchanges replaced by zero rows of the same shapes
+(``_fake_xchg``), plus the message bytes that rank would receive.  The
+projection adds the transfers as if none overlapped compute: per exchange
+the larger neighbour's bytes / link GB/s + a per-message latency (the two
+links run concurrently); "speedup_overlapped" leaves them out.  Not an RCCL
+measurement.
 """
 import argparse
 import json
@@ -115,6 +127,38 @@ def xchg_main(world, H, W, iters):
                       "per_rank": {r: res[r] for r in sorted(res)}}, indent=1))
 
 
+def perconv_main(a):
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs()).eval().to(dev)
+    g = torch.Generator().manual_seed(1234)
+    img1 = (torch.rand(1, 3, a.H, a.W, generator=g) * 255).to(dev)
+    img2 = torch.roll(img1, -8, dims=-1)
+    res = {"image": [a.H, a.W], "iters": a.iters, "mode": "per-conv halos (default)",
+           "link_gbs": a.link_gbs, "msg_us": a.msg_us, "per_N": {}}
+    glob = RowShardedStereo._heights(a.H, model.args.n_downsample, model.args.n_gru_layers)
+    reps = 3
+    with torch.no_grad():
+        for N in (1, 2, 4, 8):
+            rs = RowShardedStereo(model, N // 2, N)
+            rs._fake_xchg = True
+            r0, r1 = rs._own_rows(glob, rs.perconv_halos())
+            rs.xchg_posts = rs.xchg_bytes = rs.xchg_link_bytes = 0
+            T = timed(lambda: rs.forward(img1, img2, iters=a.iters), reps)
+            runs = reps + 1
+            posts, link = rs.xchg_posts / runs, rs.xchg_link_bytes / runs
+            xfer = link / (a.link_gbs * 1e9) + posts * a.msg_us * 1e-6
+            res["per_N"][N] = {"rank": N // 2, "own_rows": [r0, r1], "T_compute_ms": T * 1e3,
+                               "exchanges": posts, "recv_bytes": rs.xchg_bytes / runs,
+                               "link_bytes": link, "transfer_ms_if_exposed": xfer * 1e3}
+            print(f"N={N}: {json.dumps(res['per_N'][N])}", flush=True)
+    T1 = res["per_N"][1]["T_compute_ms"]
+    for N, o in res["per_N"].items():
+        o["speedup_overlapped"] = T1 / o["T_compute_ms"]
+        o["speedup_exposed"] = T1 / (o["T_compute_ms"] + o["transfer_ms_if_exposed"])
+    print(json.dumps(res, indent=1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=32)
@@ -124,7 +168,13 @@ def main():
     ap.add_argument("--W", type=int, default=2880)
     ap.add_argument("--xchg", action="store_true", help="exposed-exchange rehearsal (gloo, CPU)")
     ap.add_argument("--world", type=int, default=3)
+    ap.add_argument("--perconv", action="store_true",
+                    help="the per-conv default, whole forward per rank + transfer estimate")
+    ap.add_argument("--link-gbs", type=float, default=153.0, help="xGMI GB/s per link")
+    ap.add_argument("--msg-us", type=float, default=15.0, help="latency per exchange (us)")
     a = ap.parse_args()
+    if a.perconv:
+        return perconv_main(a)
     if a.xchg:
         return xchg_main(a.world, 768 if a.H == 1984 else a.H, 256 if a.W == 2880 else a.W,
                          8 if a.iters == 32 else a.iters)
