@@ -233,11 +233,15 @@ void lookup_kernel(LookupArgs a) {
 // the fused loop step every wave reads the pixel's coords before the block
 // barrier and only wave 0 writes the advanced coords and flow after it (the
 // outputs may alias coords1).
-template <int R, bool BF16>
+// XA: pixel blocks placed XCD by XCD (xcd_remap), so each XCD looks up one
+// contiguous eighth of the rows -- the rows whose pyramid lines the build
+// (xcd_remap'd by row) wrote through that XCD's L2.
+template <int R, bool BF16, bool XA = true>
 __global__ __launch_bounds__(256) void lookup_levelpar_kernel(LookupArgs a) {
     constexpr int T = 2 * R + 1;
     const int i = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // this wave's level
-    const long long pblk = (long long)blockIdx.x * 64;
+    const int blk = XA ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const long long pblk = (long long)blk * 64;
     const long long p = pblk + (threadIdx.x & 63);
     const bool active = p < a.P;
     const long long pp = active ? p : a.P - 1;
@@ -1486,6 +1490,10 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
             else launch_k<R, 3, false, true, 64>(a, s);
         }
 #ifdef RAFTCORR_DEV
+    } else if (variant == 6 && a.P < kLevelParP && a.levels <= 4) {   // blocks in launch order
+        const unsigned nblk = (unsigned)((a.P + 63) / 64);
+        if (bf16) hipLaunchKernelGGL((lookup_levelpar_kernel<R, true, false>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
+        else hipLaunchKernelGGL((lookup_levelpar_kernel<R, false, false>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
     } else if (variant == 1) {
         if (bf16) launch_k<R, 0, true, false>(a, s);
         else launch_k<R, 0, false, false>(a, s);
