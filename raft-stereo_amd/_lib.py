@@ -93,7 +93,7 @@ def lib():
     return _lib
 
 
-class dev_library:
+class _DevLibrary:
     """``with _lib.dev_library():`` routes every call to libraftcorr_dev.so
     (the knob-enabled A/B build) for the duration of the block."""
 
@@ -108,6 +108,9 @@ class dev_library:
         global _active
         _active = self._prev
         return False
+
+
+dev_library = _DevLibrary
 
 
 def check(rc, what):

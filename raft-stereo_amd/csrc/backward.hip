@@ -930,24 +930,19 @@ __global__ __launch_bounds__(256, 2) void volume_bwd_split_kernel(BuildBwdArgs a
     else volume_bwd_split_tile<VEC, NLEV, KM, false>(a, smem, row, tile, T1);
 }
 
+#ifdef RAFTCORR_DEV
+#include "dev/backward_dev.inc"   // A/B variants: libraftcorr_dev.so only
+#endif
+
 }  // namespace rc
 
 hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
-    if (a.levels >= 2 && a.g[1] == nullptr) {   // pair-folded gradient buffers (levels 0, 2)
 #ifdef RAFTCORR_DEV
-        // dev A/B: 21/22 occupancy floors 3/4 waves per SIMD, 23 pairs in
-        // sequence, 24 both (sequence + 4 waves)
-        const int pv = rc::dev_knob("RAFTCORR_LOOKUP_BWD_VARIANT");
-        if (pv >= 21 && pv <= 24 && radius == 4 && a.levels == 4) {
-            if (pv == 21) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
-            if (pv == 22) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 4>), dim3(nblk), dim3(256), 0, s, a);
-            if (pv == 23) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-            if (pv == 24) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<4, 4, 4, true>), dim3(nblk), dim3(256), 0, s, a);
-            return hipGetLastError();
-        }
+    if (const hipError_t e = rc::dev_launch_lookup_bwd(a, radius, nblk, s); e != hipErrorNotSupported) return e;
 #endif
+    if (a.levels >= 2 && a.g[1] == nullptr) {   // pair-folded gradient buffers (levels 0, 2)
 #define RC_LBWDP(RR)                                                                                 \
     if (a.levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<RR, 4>), dim3(nblk), dim3(256), 0, s, a); \
     else hipLaunchKernelGGL((rc::lookup_bwd_pair_kernel<RR, 2>), dim3(nblk), dim3(256), 0, s, a);
@@ -961,24 +956,7 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
 #undef RC_LBWDP
         return hipGetLastError();
     }
-#ifdef RAFTCORR_DEV
-    // dev library A/B: RAFTCORR_LOOKUP_BWD_VARIANT=1 forces the per-level-wait kernel
-    const int variant = rc::dev_knob("RAFTCORR_LOOKUP_BWD_VARIANT");
-    if (variant >= 3 && variant <= 7 && radius == 4 && a.levels == 4) {
-        // 7: non-temporal output-gradient loads (read once)
-        // 6: chunks up front, output gradients loaded per level
-        if (variant == 6) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 8, true>), dim3(nblk), dim3(256), 0, s, a);
-        if (variant == 7) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 8, false, true>), dim3(nblk), dim3(256), 0, s, a);
-        // 3: occupancy cap 3 waves/SIMD; 4 / 5: one / two levels prefetched ahead
-        if (variant == 3) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
-        if (variant == 4) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 1>), dim3(nblk), dim3(256), 0, s, a);
-        if (variant == 5) hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<4, 4, 1, 2>), dim3(nblk), dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
-#else
-    const int variant = 0;
-#endif
-    if (variant == 0 && radius >= 1 && radius <= 4 && a.levels >= 1 && a.levels <= 4) {
+    if (radius >= 1 && radius <= 4 && a.levels >= 1 && a.levels <= 4) {
 #define RC_LBWD(RR)                                                                                      \
     switch (a.levels) {                                                                                  \
         case 1: hipLaunchKernelGGL((rc::lookup_bwd_pre_kernel<RR, 1>), dim3(nblk), dim3(256), 0, s, a); break; \
@@ -1011,9 +989,6 @@ hipError_t rc_launch_lookup_bwd(const rc::LookupBwdArgs &a, int radius, hipStrea
 
 hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a_in, hipStream_t s) {
     rc::BuildBwdArgs a = a_in;
-#ifdef RAFTCORR_DEV
-    a.dev_only = rc::dev_knob("RAFTCORR_VBWD_ONLY");
-#endif
     const long long nwg = (long long)a.B * a.H * a.tm * (a.tn1 + a.tn2);
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
@@ -1030,13 +1005,12 @@ hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a_in, hipStream_t s) {
     const bool fits = (long long)a.D * a.H * (a.W1 > a.W2 ? a.W1 : a.W2) * 4 < 0xFFFFFF00LL &&
                       (Prow * a.ld[0] + a.shadow[0]) * 4 < 0xFFFFFF00LL &&
                       (!pairfold || (Prow * a.ld[2] + a.shadow[2]) * 4 < 0xFFFFFF00LL);
-    if (!a.exact && vec && fits && (pairfold || a.nlev == 1 || a.nlev == 2)) {
+    const bool split = !a.exact && vec && fits && (pairfold || a.nlev == 1 || a.nlev == 2);
 #ifdef RAFTCORR_DEV
-        if (pairfold && rc::dev_knob("RAFTCORR_VBWD_VARIANT") == 2) {   // dev A/B: G^T staged by scattered loads
-            hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, rc::kPairFold, false>), grid, blk, 0, s, a, (int)nwg);
-            return hipGetLastError();
-        }
+    if (const hipError_t e = rc::dev_launch_volume_bwd(a, split, vec, pairfold, nwg, s); e != hipErrorNotSupported)
+        return e;
 #endif
+    if (split) {
         if (pairfold) hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, rc::kPairFold>), grid, blk, 0, s, a, (int)nwg);
         else if (a.nlev == 1) hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, 1>), grid, blk, 0, s, a, (int)nwg);
         else hipLaunchKernelGGL((rc::volume_bwd_split_kernel<true, 2>), grid, blk, 0, s, a, (int)nwg);
@@ -1052,23 +1026,10 @@ hipError_t rc_launch_volume_bwd(const rc::BuildBwdArgs &a_in, hipStream_t s) {
     // three workgroups share a CU (784 vs 906 us for 32-k stages at config 2,
     // the same bits)
     if (a.nlev == 3 && a.g[1] == nullptr) {
-#ifdef RAFTCORR_DEV
-        if (vec && rc::dev_knob("RAFTCORR_VBWD_VARIANT") == 32) {   // dev A/B: 32-k stages (82 KB LDS)
-            hipLaunchKernelGGL((rc::volume_bwd_kernel<true, rc::kPairFold, 32>), grid, blk, 0, s, a, (int)nwg);
-            return hipGetLastError();
-        }
-#endif
         if (vec) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, rc::kPairFold, 16>), grid, blk, 0, s, a, (int)nwg);
         else hipLaunchKernelGGL((rc::volume_bwd_kernel<false, rc::kPairFold, 16>), grid, blk, 0, s, a, (int)nwg);
         return hipGetLastError();
     }
-#ifdef RAFTCORR_DEV
-    if (vec && rc::dev_knob("RAFTCORR_VBWD_VARIANT") == 32 && (a.nlev == 1 || a.nlev == 2)) {   // dev A/B
-        if (a.nlev == 1) hipLaunchKernelGGL((rc::volume_bwd_kernel<true, 1, 32>), grid, blk, 0, s, a, (int)nwg);
-        else hipLaunchKernelGGL((rc::volume_bwd_kernel<true, 2, 32>), grid, blk, 0, s, a, (int)nwg);
-        return hipGetLastError();
-    }
-#endif
     switch (a.nlev) {   // the level count fixes the fold's loads at compile time
         case 1: RC_VBWD(1) break;
         case 2: RC_VBWD(2) break;

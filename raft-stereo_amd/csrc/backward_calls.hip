@@ -504,46 +504,62 @@ __global__ __launch_bounds__(64) void lookup_bwd_calls_compact_kernel(LookupBwdC
     }
 }
 
+#ifdef RAFTCORR_DEV
+#include "dev/backward_calls_dev.inc"   // A/B variants: libraftcorr_dev.so only
+#endif
+
 }  // namespace rc
 
-// LDS per workgroup: pair k holds pix rows of S_k = round4(W_2k) + M floats
-// after a leading margin M = 4r+4 (the strips' reach past either end of a
-// row); pix is the largest of 64/(NL/2), ..., 8 pixels whose rows fit 64 KB.
-// Whether the fused kernels serve a whole request of n_calls calls (coords
-// batch strides cbs[0..n_calls)) on a.P / a.HW / a.W: the per-call buffer
-// resources address each output gradient and coords tensor with 32-bit
-// offsets, and a block's rows must fit 64 KB of LDS (compact rows, else whole
-// rows).  rc_corr_lookup_backward_calls asks this once, before any launch,
-// and otherwise takes the per-call path for the whole request.
-bool rc_lookup_bwd_calls_fits(const rc::LookupBwdCallsArgs &a, int radius, int levels, const long *cbs,
-                              int n_calls) {
-    if ((levels != 2 && levels != 4) || radius < 1 || radius > 4) return false;
-    if (a.P * levels * (2 * radius + 1) * 4 >= 0xFFFFFF00LL) return false;
+// The one geometry decision of the all-calls backward (asked by
+// rc_lookup_bwd_calls_fits before any launch and followed by the launcher,
+// so the two cannot drift apart): 1 = compact rows (one wave per block,
+// ``budget`` floats of LDS: twice the widest lane range W + 8R + 24 and at
+// least 20 KB), 2 = whole rows (64 KB of LDS at >= 8 pixels per block), 0 =
+// neither fits, or a per-call buffer offset would pass 32 bits.  Compact
+// rows are the default (buffer loads per call: 527 vs 681 us for whole rows
+// at W2 = 240, 1195 vs 2591 at W2 = 720, r03w/r03y); ``whole`` asks for
+// whole rows.
+static int bwd_calls_layout(const rc::LookupBwdCallsArgs &a, int radius, int levels, const long long *cbs,
+                            int n_calls, bool whole = false) {
+    if ((levels != 2 && levels != 4) || radius < 1 || radius > 4) return 0;
+    if (a.P * levels * (2 * radius + 1) * 4 >= 0xFFFFFF00LL) return 0;
     for (int c = 0; c < n_calls; ++c)
-        if (((a.P / a.HW - 1) * (long long)cbs[c] + a.HW) * 4 >= 0xFFFFFF00LL) return false;
+        if (((a.P / a.HW - 1) * cbs[c] + a.HW) * 4 >= 0xFFFFFF00LL) return 0;
     const int np = levels / 2, M = 4 * radius + 4;
     int maxS = 0, per_pix = 0;
     for (int k = 0; k < np; ++k) {
         maxS = std::max(maxS, ((a.W[2 * k] + 8 * radius + 24) + 3) & ~3);
         per_pix += ((a.W[2 * k] + 3) & ~3) + M;
     }
-    if ((long long)std::max(5120, 2 * maxS) * 4 <= 65536) return true;     // compact rows
-    return (long long)(per_pix * 8 + np * M) * 4 <= 65536;                 // whole rows, 8 pixels
+    if (!whole && (long long)std::max(5120, 2 * maxS) * 4 <= 65536) return 1;
+    return (long long)(per_pix * 8 + np * M) * 4 <= 65536 ? 2 : 0;
+}
+
+// Whether rc_launch_lookup_bwd_calls can take a request: radius 1-4, 2 or 4
+// levels, 32-bit per-call offsets, and a block's rows in 64 KB of LDS.
+// rc_corr_lookup_backward_calls asks this once, before any launch, and
+// otherwise takes the per-call path for the whole request.
+bool rc_lookup_bwd_calls_fits(const rc::LookupBwdCallsArgs &a, int radius, int levels, const long *cbs,
+                              int n_calls) {
+    long long c64[rc::kMaxBwdCalls];
+    for (int c0 = 0; c0 < n_calls; c0 += rc::kMaxBwdCalls) {
+        const int n = std::min(rc::kMaxBwdCalls, n_calls - c0);
+        for (int c = 0; c < n; ++c) c64[c] = cbs[c0 + c];
+        if (!bwd_calls_layout(a, radius, levels, c64, n)) return false;
+    }
+    return true;
 }
 
 hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int levels, hipStream_t s) {
     if (a.P <= 0 || a.ncalls <= 0) return hipSuccess;
-    if (a.ncalls > rc::kMaxBwdCalls || (levels != 2 && levels != 4) || radius < 1 || radius > 4)
-        return hipErrorInvalidValue;
-    // per-call buffer resources address each output gradient and coords
-    // tensor with 32-bit offsets (larger ones: the caller's per-call path)
-    if (a.P * levels * (2 * radius + 1) * 4 >= 0xFFFFFF00LL) return hipErrorNotSupported;
-    for (int c = 0; c < a.ncalls; ++c)
-        if (((a.P / a.HW - 1) * a.cbs[c] + a.HW) * 4 >= 0xFFFFFF00LL) return hipErrorNotSupported;
-    {
-        // compact rows: one wave per block, `budget` floats of LDS: at least
-        // twice the widest possible lane range (W + 8R + 24) and 20 KB
-        // (8 blocks per CU)
+    if (a.ncalls > rc::kMaxBwdCalls) return hipErrorInvalidValue;
+    bool whole = false;
+#ifdef RAFTCORR_DEV
+    whole = rc::dev_bwdc_whole_rows(radius, levels);
+#endif
+    const int layout = bwd_calls_layout(a, radius, levels, a.cbs, a.ncalls, whole);
+    if (layout == 0) return hipErrorNotSupported;
+    if (layout == 1) {
         const int np = levels / 2;
         int maxS = 0;
         for (int k = 0; k < np; ++k) {
@@ -552,29 +568,19 @@ hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int
         }
         a.budget = std::max(5120, 2 * maxS);
         a.pix = 64 / np;
-        // compact rows by default (with buffer loads per call: 527 vs 681 us
-        // for whole rows at W2 = 240, 1195 vs 2591 at W2 = 720, r03w/r03y)
-        bool use_compact = true;
-#ifdef RAFTCORR_DEV
-        const int dv = rc::dev_knob("RAFTCORR_BWDC_VARIANT");   // dev A/B: 0 = the launcher's choice,
-        if (dv == 3) use_compact = true;                         // 3 = compact, 1 / 2 = whole rows
-        if (dv == 1 || dv == 2) use_compact = false;
-#endif
-        if (use_compact && (long long)a.budget * 4 <= 65536) {
-            const unsigned nblk = (unsigned)((a.P + a.pix - 1) / a.pix);
-            const size_t lds = (size_t)a.budget * 4;
+        const unsigned nblk = (unsigned)((a.P + a.pix - 1) / a.pix);
+        const size_t lds = (size_t)a.budget * 4;
 #define RC_LBWDCC(RR)                                                                                                 \
     if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_compact_kernel<RR, 4>), dim3(nblk), dim3(64), lds, s, a); \
     else hipLaunchKernelGGL((rc::lookup_bwd_calls_compact_kernel<RR, 2>), dim3(nblk), dim3(64), lds, s, a);
-            switch (radius) {
-                case 1: RC_LBWDCC(1) break;
-                case 2: RC_LBWDCC(2) break;
-                case 3: RC_LBWDCC(3) break;
-                case 4: RC_LBWDCC(4) break;
-            }
-#undef RC_LBWDCC
-            return hipGetLastError();
+        switch (radius) {
+            case 1: RC_LBWDCC(1) break;
+            case 2: RC_LBWDCC(2) break;
+            case 3: RC_LBWDCC(3) break;
+            case 4: RC_LBWDCC(4) break;
         }
+#undef RC_LBWDCC
+        return hipGetLastError();
     }
 
     const int np = levels / 2, M = 4 * radius + 4;
@@ -599,13 +605,8 @@ hipError_t rc_launch_lookup_bwd_calls(rc::LookupBwdCallsArgs &a, int radius, int
     const size_t lds = (size_t)a.lds_floats * 4;
     const dim3 blk(pix * np);
 #ifdef RAFTCORR_DEV
-    // dev A/B: RAFTCORR_BWDC_VARIANT=1 runs the whole-row pipelined kernel,
-    // 2 the whole-row unpipelined form (two read-modify-writes per call)
-    if (rc::dev_knob("RAFTCORR_BWDC_VARIANT") == 2 && radius == 4) {
-        if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<4, 4, false>), dim3(nblk), blk, lds, s, a);
-        else hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<4, 2, false>), dim3(nblk), blk, lds, s, a);
-        return hipGetLastError();
-    }
+    if (const hipError_t e = rc::dev_launch_bwdc_whole(a, radius, levels, nblk, blk, lds, s); e != hipErrorNotSupported)
+        return e;
 #endif
 #define RC_LBWDC(RR)                                                                                      \
     if (levels == 4) hipLaunchKernelGGL((rc::lookup_bwd_calls_kernel<RR, 4>), dim3(nblk), blk, lds, s, a); \

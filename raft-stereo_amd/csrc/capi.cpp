@@ -54,14 +54,6 @@ bool is_pow2_float(float v) {
 }
 }  // namespace
 
-#ifdef RAFTCORR_DEV
-namespace {
-unsigned long long *g_dbg = nullptr;   // stamp buffer of the diagnostic kernels
-}
-// Dev library only: device buffer the diagnostic (stamped) kernel variants
-// write their per-wave timelines to (tools/lookup_timeline.py); NULL = none.
-extern "C" void rc_dev_set_dbg(void *p) { g_dbg = static_cast<unsigned long long *>(p); }
-#endif
 
 extern "C" int rc_abi_version(void) { return RC_ABI_VERSION; }
 
@@ -226,9 +218,6 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
     a.coords = coords_x;
     a.cbs = coord_batch_stride;
     a.P = P;
-#ifdef RAFTCORR_DEV
-    a.dbg = g_dbg;
-#endif
     a.HW = H * W1;
     a.levels = levels;
     return RC_OK;

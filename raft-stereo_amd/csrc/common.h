@@ -140,7 +140,6 @@ struct LookupArgs {
     const float *delta;
     float *coords_out;
     float *flow_out;
-    unsigned long long *dbg;  // dev library only: per-wave timeline stamps (else null)
     // line-phase shadow copy of level i at (char*)lvl[i] + shadow[i] bytes
     // (0 = none); read by the pair kernel (RC_SHADOW, ABI v5)
     long long shadow[kMaxLevels];
@@ -205,9 +204,6 @@ struct BuildBwdArgs {
 // Host-side launchers (defined in the .hip files, called by capi.cpp).
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s);
 hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s);     // may lower a.nfused
-hipError_t rc_launch_build_split8(const rc::BuildArgs &a, hipStream_t s);   // hipErrorNotSupported: not taken
-hipError_t rc_launch_build_split_persist(const rc::BuildArgs &a, long long ntiles, int tf1, int tf2, int tiles1,
-                                         int tiles2, hipStream_t s);   // hipErrorNotSupported: not taken
 hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s);   // may lower a.nfused
 hipError_t rc_launch_pool(const void *in, long long ld_in, void *out, long long ld_out, long rows,
                           int W_in, int bf16, hipStream_t s);

@@ -12,7 +12,7 @@
 // padding), so they need not be written.
 #include <stdlib.h>
 
-#include "common.h"
+#include "../common.h"
 
 namespace rc {
 

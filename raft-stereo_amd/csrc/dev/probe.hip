@@ -19,7 +19,7 @@
 // predication).  The lane writes the xor of everything it loaded, so no load
 // is dead.  Rows are taken modulo `nrows` (nrows < lanes re-reads rows: a
 // small table is cache-served).
-#include "common.h"
+#include "../common.h"
 
 namespace rc {
 

@@ -12,11 +12,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Dev-only ablation flags (RAFTCORR_BUILD_MODE): 1 = no operand loads,
 // 2 = no epilogue stores.  Product launches use 0.
 enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8, kModeNoFragReads = 16,
-       kModeStagger = 64, kModeSched = 128, kModeReorder = 256,
-       kModeNoMfma = 512, kModeNoSplit = 1024, kModeSpread = 2048, kModePackedSub = 8192,
-       kMode32 = 16384, kModePhase = 32768, kModeL2Stores = 65536,
-       kModeDirect = 131072, kModeFastEpi = 262144, kModeGenericEpi = 524288,
-       kModePairEpi = 1048576, kModeOldAddr = 2097152 };
+       kModeStagger = 64, kModeNoMfma = 512, kModeNoSplit = 1024, kModeSpread = 2048, kModePackedSub = 8192,
+       kModeL2Stores = 65536, kModeDirect = 131072, kModeFastEpi = 262144, kModeGenericEpi = 524288,
+       kModePairEpi = 1048576 };
 
 // VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
 template <int VW>

@@ -504,130 +504,7 @@ __device__ __forceinline__ void tap_span(float xl, int W, int &f, int &l) {
     l = min((int)floorf(pb) + 1, W - 1);
 }
 
-#ifdef RAFTCORR_DEV
-// Level-0 chain (dev variant 220): every level 0..NL-1
-// derived from ONE span of level 0 -- the top level's 2r+4 window scaled by
-// S = 2^(NL-1) (96 elements at L = 4, r = 4), exact-span predicated -- so the
-// lookups read level 0 only (249 MB at config 2 instead of levels 0 + 2 and the
-// level-2 copy) at the cost of more 64-B sectors per pixel (4.7 vs 3.7
-// simulated).  Level i window element jj is the pool_tree of 2^i level-0
-// elements, the fp32 ops of avg_pool2d applied i times (model.py:294).
-template <int R, int NL>
-__global__ __launch_bounds__(256) void lookup_l0chain_kernel(LookupArgs a) {
-    constexpr int T = 2 * R + 1, NW = 2 * R + 4, TOP = NL - 1, S = 1 << TOP;
-    constexpr int NE0 = S * NW, NC0 = NE0 / 4;
-    static_assert(S % 4 == 0, "span start must be 16-B aligned");
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const long long pblk = (long long)blk * 256;
-    const long long p = pblk + threadIdx.x;
-    const bool active = p < a.P;
-    const long long pp = active ? p : a.P - 1;
-    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
-    const float x = pixel_x(a, bimg, rem, active);
-    float *outp = a.out + bimg * (long long)(NL * T) * a.HW + rem;
-    const long long lrow = pp - pblk;
-    const float xtop = x / (float)(1 << TOP);
-    const bool inwin = (xtop > -(float)(R + 4)) && (xtop < (float)(a.W[TOP] + R + 4));
-    const float ntop = inwin ? floorf(xtop) : 0.0f;
-    const int e0 = S * ((int)ntop - R - 1);
-    int lo = 0x7FFFFFFF, hi = -1;
-    if (inwin) {
-#pragma unroll
-        for (int i = 0; i <= TOP; ++i) {
-            int f, l;
-            tap_span<R>(x / (float)(1 << i), a.W[i], f, l);
-            if (f <= l) {
-                lo = min(lo, f << i);
-                hi = max(hi, ((l + 1) << i) - 1);
-            }
-        }
-    }
-    const long long ld0 = a.ld[0];
-    const float *lvl0 = static_cast<const float *>(a.lvl[0]);
-    const auto rs0 = make_rsrc(lvl0 + pblk * ld0, clamp_bytes((a.P - pblk) * ld0 * 4));
-    float s0[NE0];
-#pragma unroll
-    for (int k = 0; k < NC0; ++k) {
-        const int cs = e0 + 4 * k;
-        const bool ok = cs <= hi && cs + 3 >= lo;
-        const f32x4 v = ld4(rs0, ok ? (uint32_t)((lrow * ld0 + cs) * 4) : 0xFFFFFF00u);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) s0[4 * k + c] = v[c];
-    }
-    const float *row0 = lvl0 + pp * ld0;
-    auto level = [&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        constexpr int SI = 1 << i, NDD = 1 << (TOP - i);
-        const int W = a.W[i];
-        const float Wm1 = (float)(W - 1), half = Wm1 / 2.0f;
-        const DivRN dv = div_prep(Wm1);
-        const float xl = x / (float)(1 << i);
-        const float n = inwin ? floorf(xl) : 0.0f;
-        const int dd = inwin ? (int)n - NDD * (int)ntop : 0;
-        const bool valid = inwin && dd >= 0 && dd < NDD;
-        float w[NW];
-#pragma unroll
-        for (int jj = 0; jj < NW; ++jj) {
-            float val = 0.0f;
-#pragma unroll
-            for (int d = 0; d < NDD; ++d) {
-                constexpr int base = (R + 1) * (S - SI);
-                const float v = pool_tree<SI>(s0 + base + SI * (d + jj));
-                val = (dd == d) ? v : val;
-            }
-            w[jj] = val;
-        }
-        float res[T];
-        bool bad = false;
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            const float xt = (float)(t - R) + xl;
-            const float xn = div_rn(2.0f * xt, dv) - 1.0f;
-            const float xp = (xn + 1.0f) * half;
-            const float x0 = floorf(xp);
-            const float w1 = xp - x0, w0 = 1.0f - w1;
-            const float nt = n + (float)(t - R);
-            const bool lo_ = x0 < nt, hi_ = x0 > nt;
-            float e0_ = w[t], e1_ = w[t + 1], e2_ = w[t + 2], e3_ = w[t + 3];
-            asm("" : "+v"(e0_), "+v"(e1_), "+v"(e2_), "+v"(e3_));
-            const float a0 = lo_ ? e0_ : (hi_ ? e2_ : e1_);
-            const float a1 = lo_ ? e1_ : (hi_ ? e3_ : e2_);
-            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
-            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
-            bad |= inwin && (!valid || x0 < nt - 1.0f || x0 > nt + 1.0f);
-            res[t] = fmaf(w1, ok1 ? a1 : 0.0f, w0 * (ok0 ? a0 : 0.0f));
-        }
-        if (__builtin_expect(bad, 0)) {
-            for (int t = 0; t < T; ++t) {
-                const float xt = (float)(t - R) + xl;
-                const float xn = div_rn(2.0f * xt, dv) - 1.0f;
-                const float xp = (xn + 1.0f) * half;
-                const float x0 = floorf(xp);
-                const float w1 = xp - x0, w0 = 1.0f - w1;
-                const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
-                const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
-                const float v0 = ok0 ? derived_elem<SI>(row0, (long long)x0) : 0.0f;
-                const float v1 = ok1 ? derived_elem<SI>(row0, (long long)x0 + 1) : 0.0f;
-                res[t] = fmaf(w1, v1, w0 * v0);
-            }
-        }
-        if (active) {
-#pragma unroll
-            for (int t = 0; t < T; ++t) outp[(long long)(i * T + t) * a.HW] = res[t];
-        }
-    };
-    level(std::integral_constant<int, 0>{});
-    level(std::integral_constant<int, 1>{});
-    level(std::integral_constant<int, 2>{});
-    if constexpr (TOP >= 3) level(std::integral_constant<int, 3>{});
-}
-#endif
-
-// PH (dev-only timing probes; the values read are NOT the span's): 1 = read
-// each span at +64 B when that touches fewer 128-B lines (what a second,
-// half-line-shifted copy of the level would give), 2 = move every span to a
-// 128-B line start (lower bound: the fewest lines any layout could give).
-template <int R, bool BF16 = false, int PH = 0>
+template <int R, bool BF16 = false>
 __device__ __forceinline__ void issue_pair(PairSpan<R, BF16> &ps, const LookupArgs &a, int lo, float x,
                                            long long pblk, long long lrow) {
     typedef PairSpan<R, BF16> PS;
@@ -658,20 +535,14 @@ __device__ __forceinline__ void issue_pair(PairSpan<R, BF16> &ps, const LookupAr
     const long long shb = a.shadow[lo];
     const auto rs = make_rsrc(lvl + pblk * ld * PS::ES, clamp_bytes((a.P - pblk) * ld * PS::ES + shb));
     uint32_t phase = 0;
-    if (shb != 0 || PH != 0) {
+    if (shb != 0 && lo_e <= hi_e) {
         const unsigned long long b0 =
             (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + (lo_e & ~(PS::EPC - 1))) * PS::ES);
         const unsigned long long b1 = (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + hi_e) * PS::ES);
-        if (lo_e <= hi_e) {
-            if constexpr (PH == 2) {     // dev probe: line-aligned spans
-                phase = (uint32_t)((128 - (b0 & 127)) & 127);
-            } else {
-                const unsigned long long sh = PH == 1 ? 64ull : (unsigned long long)shb;
-                const long long l0 = (long long)(b1 >> 7) - (long long)(b0 >> 7);
-                const long long l1 = (long long)((b1 + sh) >> 7) - (long long)((b0 + sh) >> 7);
-                phase = l1 < l0 ? (uint32_t)sh : 0u;
-            }
-        }
+        const unsigned long long sh = (unsigned long long)shb;
+        const long long l0 = (long long)(b1 >> 7) - (long long)(b0 >> 7);
+        const long long l1 = (long long)((b1 + sh) >> 7) - (long long)((b0 + sh) >> 7);
+        phase = l1 < l0 ? (uint32_t)sh : 0u;
     }
 #pragma unroll
     for (int k = 0; k < PS::NC; ++k) {
@@ -835,13 +706,11 @@ __device__ __forceinline__ PairPixel pair_pixel(const LookupArgs &a, long long p
 // stores through a per-wave LDS tile (9 instead of 36 store instructions per
 // wave: 26.0 vs 25.8 us), two pixels per lane with both pixels' loads in
 // flight (26.6 us, 198 VGPRs).
-// M: dev-only ablation (RAFTCORR_LOOKUP_VARIANT 201-204, dev library):
-// 1 = no output stores, 2 = no fallback path, 3 / 4 = issue_pair's line-phase
-// probes PH 1 / 2 (timing only: wrong values), 5 = hardware block order
-// (no XCD remap; same values), 6 = PH 1, 7 = non-temporal output stores;
-// the WPE parameter (dev variants 208/209) caps registers for 5/6 waves/SIMD;
-// 9 (variant 211) = the channels-last store path writing into an NCHW
-// buffer (timing A/B of the two layouts on the same output tensor).
+// M: ablation modes (dev library only, dev/lookup_dev.inc): 1 = no output
+// stores, 2 = no fallback path, 5 = hardware block order (no XCD remap; same
+// values), 7 = non-temporal output stores, 9 = the channels-last store path
+// writing into an NCHW buffer (timing A/B of the two layouts); WPE caps
+// registers for 5/6 waves/SIMD.
 template <int R, int NL, int M = 0, bool BF16 = false, int WPE = 1, bool CL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_pair_kernel(LookupArgs a) {
     static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
@@ -854,7 +723,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     PairSpan<R, BF16> sp[NP];
 #pragma unroll
     for (int k = 0; k < NP; ++k)
-        issue_pair<R, BF16, (M == 3 || M == 6) ? 1 : (M == 4 ? 2 : 0)>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
+        issue_pair<R, BF16>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
     constexpr int C = NL * (2 * R + 1);
     // CL: channels-last output (RC_OUT_CHANNELS_LAST), out[p*C + ch].  A
     // wave's 64 pixels own one contiguous run of 64*C floats; it is gathered
@@ -896,489 +765,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
-#ifdef RAFTCORR_DEV
-// Disparity-major ("sheared") pair lookup (dev only): the
-// pair kernel's arithmetic (levels 0 and 2 stored, 1 and 3 their pairwise
-// means, finish_pair) over levels stored as S_i[b,h][k][w1] with
-// k = (w1 >> i) - j + W_i - 1 (lookup_sheared.hip's layout), so the lanes of
-// a wave whose pixels look at the same disparity read one contiguous run of
-// a row per span element -- coalesced along w1 -- instead of a 16-B piece of
-// 64 different pixel rows.  A span is 2(2r+4) dword loads per lane (exact-
-// span predicated).  No memory fallback (finish_pair NOFALLBACK): the probe
-// feeds no subnormal coordinates.
-template <int R>
-__global__ __launch_bounds__(256) void lookup_sheared_pair_kernel(LookupArgs a, const float *s0, const float *s2,
-                                                                  long long K0, long long K2, long long ldw) {
-    constexpr int NS = PairSpan<R>::NS;
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const long long pblk = (long long)blk * 256;
-    const long long p = pblk + threadIdx.x;
-    const bool active = p < a.P;
-    const long long pp = active ? p : a.P - 1;
-    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
-    const float x = pixel_x(a, bimg, rem, active);
-    const int H = a.HW / a.W1;
-    const int h = (int)(rem / a.W1), w1 = (int)(rem - (long long)h * a.W1);
-    const long long bh = bimg * H + h, bh0 = pblk / a.W1;          // bh0: block-uniform
-    float *outp = a.out + bimg * (long long)(4 * (2 * R + 1)) * a.HW + rem;
-    auto sink = [&](int ch, float v) {
-        if (active) outp[(long long)ch * a.HW] = v;
-    };
-    PairSpan<R> sp[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int lo = 2 * k;
-        PairSpan<R> &ps = sp[k];
-        const int Wlo = a.W[lo], Whi = a.W[lo + 1];
-        const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
-        ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));
-        ps.m = ps.inwin ? floorf(xhi) : 0.0f;
-        ps.n = ps.inwin ? floorf(xlo) : 0.0f;
-        const int dd = (int)ps.n - 2 * (int)ps.m;
-        ps.valid = ps.inwin && (dd == 0 || dd == 1);
-        int lo_e = 0x7FFFFFFF, hi_e = -1;
-        if (ps.inwin) {
-            int f, l;
-            tap_span<R>(xlo, Wlo, f, l);
-            if (f <= l) { lo_e = f; hi_e = l; }
-            tap_span<R>(xhi, Whi, f, l);
-            if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
-        }
-        ps.sh = 0;
-        const int sa = 2 * ((int)ps.m - R - 1);
-        const long long K = k ? K2 : K0;
-        const float *lv = k ? s2 : s0;
-        const auto rs = make_rsrc(lv + bh0 * K * ldw, clamp_bytes((a.P / a.W1 - bh0) * K * ldw * 4));
-        const long long rowk = (bh - bh0) * K + (w1 >> lo) + Wlo - 1;    // row of element 0
-#pragma unroll
-        for (int c = 0; c < PairSpan<R>::NC * 4; ++c) {
-            const int j = sa + c;
-            const bool ok = c < NS && j >= lo_e && j <= hi_e;
-            const uint32_t off = ok ? (uint32_t)(((rowk - j) * ldw + w1) * 4) : 0xFFFFFF00u;
-            ps.q[c >> 2][c & 3] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) finish_pair<R, true>(sp[k], a, 2 * k, x, pp, sink);
-}
-#endif
-
-// Persistent pair lookup (dev variants 215-219 while measured).  The one-round
-// grid of lookup_pair_kernel puts every wave in the same phase: all spans are
-// requested at launch and each wave's output stores follow its own loads.
-// Here each wave walks 64-pixel groups g, g + S, g + 2S, ... of its XCD's
-// contiguous share of the image (S = waves on that XCD), and with PIPE the
-// spans of group n+1 are requested before group n's tap math and stores, so a
-// wave's stores overlap its own next loads; the x of group n+2 is loaded one
-// stage ahead, so issuing the next spans never waits on the current ones.
-// Same PairSpan / finish_pair as the pair kernel: bit-identical output.
-__device__ __forceinline__ float group_x(const LookupArgs &a, long long g, int lane) {
-    const long long p = g * 64 + lane;
-    const long long pp = p < a.P ? p : a.P - 1;
-    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
-    return pixel_x(a, bimg, rem, p < a.P);
+template <int R, int NL, bool BF16, bool EXACT, int BS = 256, int WPE = 1>
+static void launch_k(const LookupArgs &a, hipStream_t s) {
+    const unsigned nblk = (unsigned)((a.P + BS - 1) / BS);
+    hipLaunchKernelGGL((lookup_kernel<R, NL, BF16, EXACT, BS, WPE>), dim3(nblk), dim3(BS), 0, s, a);
 }
 
-template <int R, int NL, bool BF16, bool PIPE, int WPE = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_pair_persist_kernel(LookupArgs a) {
-    static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
-    constexpr int NP = NL / 2;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const long long NG = (a.P + 63) >> 6;
-    const int nb = gridDim.x, xcd = blockIdx.x & 7, kb = blockIdx.x >> 3;
-    const int nbx = (nb >> 3) + (xcd < (nb & 7) ? 1 : 0);          // blocks on this XCD
-    const long long gq = NG >> 3, gr = NG & 7;
-    const long long g0 = xcd * gq + (xcd < gr ? xcd : gr);
-    const long long g1 = g0 + gq + (xcd < gr ? 1 : 0);              // this XCD's groups [g0, g1)
-    const long long S = 4LL * nbx;
-    long long g = g0 + 4LL * kb + w;
-    if (g >= g1) return;
-    auto pix = [&](long long gg, float x) {
-        PairPixel q;
-        q.pblk = gg * 64;
-        const long long p = q.pblk + lane;
-        q.active = p < a.P;
-        q.pp = q.active ? p : a.P - 1;
-        const long long bimg = q.pp / a.HW, rem = q.pp - bimg * a.HW;
-        q.x = x;
-        q.outp = a.out + bimg * (long long)(NL * (2 * R + 1)) * a.HW + rem;
-        q.lrow = lane;
-        return q;
-    };
-    auto sink_of = [&](const PairPixel &q) {
-        return [&a, q](int ch, float v) {
-            if (q.active) q.outp[(long long)ch * a.HW] = v;
-        };
-    };
-    if constexpr (!PIPE) {
-        for (; g < g1; g += S) {
-            const PairPixel q = pix(g, group_x(a, g, lane));
-            PairSpan<R, BF16> sp[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sp[k], a, 2 * k, q.x, q.pblk, q.lrow);
-#pragma unroll
-            for (int k = 0; k < NP; ++k) finish_pair<R, false, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink_of(q));
-        }
-    } else {
-        PairPixel qa = pix(g, group_x(a, g, lane));
-        float xn = g + S < g1 ? group_x(a, g + S, lane) : 0.0f;   // x of the next group
-        PairSpan<R, BF16> sa[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sa[k], a, 2 * k, qa.x, qa.pblk, qa.lrow);
-        for (;;) {
-            const long long gn = g + S;
-            const bool more = gn < g1;                               // wave-uniform
-            PairPixel qb;
-            PairSpan<R, BF16> sb[NP];
-            if (more) {
-                const float x2 = gn + S < g1 ? group_x(a, gn + S, lane) : 0.0f;
-                qb = pix(gn, xn);
-#pragma unroll
-                for (int k = 0; k < NP; ++k) issue_pair<R, BF16>(sb[k], a, 2 * k, qb.x, qb.pblk, qb.lrow);
-                xn = x2;
-            }
-#pragma unroll
-            for (int k = 0; k < NP; ++k) finish_pair<R, false, BF16>(sa[k], a, 2 * k, qa.x, qa.pp, sink_of(qa));
-            if (!more) break;
-            qa = qb;
-#pragma unroll
-            for (int k = 0; k < NP; ++k) sa[k] = sb[k];
-            g = gn;
-        }
-    }
-}
-
-template <int R, bool PIPE, int WPE>
-static void launch_pair_persist(const LookupArgs &a, int bf16, int blocks_per_cu, hipStream_t s) {
-    const long long NG = (a.P + 63) >> 6;
-    long long nblk = 256LL * blocks_per_cu;                         // MI355X: 256 CUs
-    if (nblk * 4 > NG) nblk = (NG + 3) / 4;
-    if (a.levels == 4) {
-        if (bf16) hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 4, true, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 4, false, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
-    } else {
-        if (bf16) hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 2, true, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_persist_kernel<R, 2, false, PIPE, WPE>), dim3(nblk), dim3(256), 0, s, a);
-    }
-}
-
-// Cooperative span loads (dev variants 212-214 while measured).  The pair
-// kernel above has each lane fetch its own two spans with 7 (fp32) 16-B
-// loads: every wave-instruction then touches 64 different rows, and a span's
-// 128-B line is requested as two 64-B sectors by two different instructions.
-// Here LPS lanes load one span together (LPS x 16 B covers the span's
-// chunks), so one instruction covers 64 / LPS spans and asks for each line
-// once; the chunks land in LDS by buffer->LDS DMA (no VGPRs held while in
-// flight), and each pixel's lane reads its span back with NC ds_read_b128.
-// Same PairSpan fields and the same finish_pair, so the output is the pair
-// kernel's bit for bit.
-template <int R, bool BF16>
-struct CoopGeom {
-    typedef PairSpan<R, BF16> PS;
-    static constexpr int LPS = PS::NC <= 4 ? 4 : 8;   // lanes per span (16-B chunks)
-    static constexpr int SPI = 64 / LPS;              // spans per wave-instruction
-    static constexpr int NI = 64 / SPI;               // instructions per wave and level pair
-    static constexpr int SPAN_B = 64 * 16 * NI;       // LDS bytes per wave and level pair (1 KB per instr)
-    static_assert(PS::NC <= LPS, "span chunks exceed the lanes per span");
-    // chunk-position swizzle: lanes p and p + 8 of a ds_read_b128 lane group
-    // would hit the same banks with 8 lanes per span
-    __device__ static __forceinline__ int swz(int j) { return LPS == 8 ? (j & 1) : 0; }
-    // LDS byte offset of chunk c of the span of the wave's pixel p
-    __device__ static __forceinline__ int at(int p, int c) {
-        const int j = p / SPI;
-        return j * 1024 + ((c ^ swz(j)) * SPI + (p % SPI)) * 16;
-    }
-};
-
-// As issue_pair, but returns the span's byte offset (chunk 0) and the mask of
-// chunks to fetch instead of loading them.
-template <int R, bool BF16 = false>
-__device__ __forceinline__ uint32_t plan_pair(PairSpan<R, BF16> &ps, const LookupArgs &a, int lo, float x,
-                                              long long pblk, long long lrow) {
-    typedef PairSpan<R, BF16> PS;
-    const int Wlo = a.W[lo], Whi = a.W[lo + 1];
-    const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
-    ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));
-    ps.m = ps.inwin ? floorf(xhi) : 0.0f;
-    ps.n = ps.inwin ? floorf(xlo) : 0.0f;
-    const int dd = (int)ps.n - 2 * (int)ps.m;
-    ps.valid = ps.inwin && (dd == 0 || dd == 1);
-    int lo_e = 0x7FFFFFFF, hi_e = -1;
-    if (ps.inwin) {
-        int f, l;
-        tap_span<R>(xlo, Wlo, f, l);
-        if (f <= l) { lo_e = f; hi_e = l; }
-        tap_span<R>(xhi, Whi, f, l);
-        if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
-    }
-    const int sa = 2 * ((int)ps.m - R - 1);
-    const int ea = sa & ~(PS::EPC - 1);
-    ps.sh = sa - ea;
-    const long long ld = a.ld[lo];
-    const char *lvl = static_cast<const char *>(a.lvl[lo]);
-    const long long shb = a.shadow[lo];
-    uint32_t phase = 0;
-    if (shb != 0 && lo_e <= hi_e) {
-        const unsigned long long b0 =
-            (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + (lo_e & ~(PS::EPC - 1))) * PS::ES);
-        const unsigned long long b1 = (unsigned long long)(uintptr_t)(lvl + ((pblk + lrow) * ld + hi_e) * PS::ES);
-        const long long l0 = (long long)(b1 >> 7) - (long long)(b0 >> 7);
-        const long long l1 = (long long)((b1 + shb) >> 7) - (long long)((b0 + shb) >> 7);
-        phase = l1 < l0 ? 1u : 0u;
-    }
-    // the chunks [first, last] hold [lo_e, hi_e] (none: first > last)
-    int first = 7, last = 0;
-    if (lo_e <= hi_e) {
-        first = max((lo_e - ea) / PS::EPC, 0);
-        last = min((hi_e - ea) / PS::EPC, PS::NC - 1);
-    }
-    // packed plan: bits 0-22 the byte offset / 16 of chunk `first` (>= 0;
-    // lrow < 64, ld*ES <= 2^18: < 2^20), bit 23 shadow copy, bits 24-26 first
-    // chunk, 27-29 last chunk.  (Chunk 0 may start before the row: ea < 0.)
-    const uint32_t loc = first <= last ? (uint32_t)((lrow * ld + ea + PS::EPC * first) * PS::ES) >> 4 : 0u;
-    return loc | (phase << 23) | ((uint32_t)first << 24) | ((uint32_t)last << 27);
-}
-
-// One wave's cooperative fetch of the spans of level pair `lo` for its 64
-// pixels into `sbuf` (SPAN_B bytes): instruction j loads the spans of pixels
-// SPI*j .. SPI*j + SPI-1, lane l chunk (l / SPI) ^ swz(j) of pixel SPI*j + l % SPI.
-// Each pixel's plan travels in one dword (`pk`, see coop_pack): all the
-// wave's ds_bpermutes issue before its loads.
-template <int R, bool BF16>
-__device__ __forceinline__ void coop_fetch(const LookupArgs &a, int lo, long long pblk, uint32_t pk,
-                                           __attribute__((address_space(3))) char *sbuf) {
-    typedef CoopGeom<R, BF16> G;
-    typedef PairSpan<R, BF16> PS;
-    const int lane = threadIdx.x & 63;
-    const long long ld = a.ld[lo];
-    const uint32_t shb = (uint32_t)a.shadow[lo];
-    const auto rs = make_rsrc(static_cast<const char *>(a.lvl[lo]) + pblk * ld * PS::ES,
-                              clamp_bytes((a.P - pblk) * ld * PS::ES + a.shadow[lo]));
-    uint32_t v[G::NI];
-#pragma unroll
-    for (int j = 0; j < G::NI; ++j) v[j] = (uint32_t)__shfl((int)pk, G::SPI * j + lane % G::SPI, 64);
-#pragma unroll
-    for (int j = 0; j < G::NI; ++j) {
-        const int c = (lane / G::SPI) ^ G::swz(j);
-        const uint32_t first = (v[j] >> 24) & 7u, last = (v[j] >> 27) & 7u;
-        const uint32_t o = ((v[j] & 0x7FFFFFu) << 4) + ((v[j] >> 23) & 1u ? shb : 0u) + 16u * ((uint32_t)c - first);
-        const uint32_t off = ((uint32_t)c >= first && (uint32_t)c <= last) ? o : 0xFFFFFF00u;
-#if defined(__HIP_DEVICE_COMPILE__)   // the LDS-pointer builtin has no host form
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(sbuf + j * 1024),
-                                                 16, (int)off, 0, 0, 0);
-#else
-        (void)rs; (void)off;
-#endif
-    }
-}
-
-template <int R, bool BF16>
-__device__ __forceinline__ void coop_read(PairSpan<R, BF16> &ps, const char *sbuf) {
-    typedef CoopGeom<R, BF16> G;
-    const int p = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < PairSpan<R, BF16>::NC; ++k) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(sbuf + G::at(p, k));
-        ps.q[k][0] = v.x; ps.q[k][1] = v.y; ps.q[k][2] = v.z; ps.q[k][3] = v.w;
-    }
-}
-
-template <int R, int NL, int WPB, bool BF16 = false>
-__global__ __launch_bounds__(64 * WPB) void lookup_pair_coop_kernel(LookupArgs a) {
-    static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
-    typedef CoopGeom<R, BF16> G;
-    constexpr int NP = NL / 2;
-    __shared__ __attribute__((aligned(16))) char sbuf[WPB][NP][G::SPAN_B];
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const long long pblk = (long long)blk * 64 * WPB;
-    const PairPixel q = pair_pixel<R, NL>(a, pblk);
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const long long pw = pblk + 64 * w;             // the wave's first pixel (wave-uniform)
-    PairSpan<R, BF16> sp[NP];
-    uint32_t pk[NP];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) pk[k] = plan_pair<R, BF16>(sp[k], a, 2 * k, q.x, pw, q.pp - pw);
-#pragma unroll
-    for (int k = 0; k < NP; ++k)
-        coop_fetch<R, BF16>(a, 2 * k, pw, pk[k], (__attribute__((address_space(3))) char *)sbuf[w][k]);
-    // both spans back into registers before any output store: a store is
-    // counted in vmcnt, so a later LDS read would wait for it too
-#pragma unroll
-    for (int k = 0; k < NP; ++k) coop_read<R, BF16>(sp[k], sbuf[w][k]);
-    auto sink = [&](int ch, float v) {
-        if (q.active) q.outp[(long long)ch * a.HW] = v;
-    };
-#pragma unroll
-    for (int k = 0; k < NP; ++k) finish_pair<R, false, BF16>(sp[k], a, 2 * k, q.x, q.pp, sink);
-}
-
-template <int R, int WPB>
-static void launch_pair_coop(const LookupArgs &a, int bf16, hipStream_t s) {
-    const unsigned nblk = (unsigned)((a.P + 64 * WPB - 1) / (64 * WPB));
-    if (a.levels == 4) {
-        if (bf16) hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 4, WPB, true>), dim3(nblk), dim3(64 * WPB), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 4, WPB>), dim3(nblk), dim3(64 * WPB), 0, s, a);
-    } else {
-        if (bf16) hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 2, WPB, true>), dim3(nblk), dim3(64 * WPB), 0, s, a);
-        else hipLaunchKernelGGL((lookup_pair_coop_kernel<R, 2, WPB>), dim3(nblk), dim3(64 * WPB), 0, s, a);
-    }
-}
-
-#ifdef RAFTCORR_DEV
-__device__ __forceinline__ unsigned long long rtc_stamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-
-// Diagnostic build of the 4-level pair kernel (dev library, variant 210):
-// lane 0 of every wave records s_memrealtime (100 MHz) at
-//   0 start, 1 loads issued, 2 span 0 landed, 3 pair 0 done (math + stores
-//   issued), 4 span 2 landed, 5 pair 2 done, 6 all stores drained,
-// plus HW_ID, into dbg[wave * 8 + k].  Its run time is not the product's
-// (the waits forbid overlaps); read shares and distributions only.
-template <int R>
-__global__ __launch_bounds__(256) void lookup_pair_stamped_kernel(LookupArgs a) {
-    unsigned long long st[7];
-    st[0] = rtc_stamp();
-    const PairPixel q = pair_pixel<R, 4>(a, (long long)blockIdx.x * 256);
-    PairSpan<R> s0, s2;
-    issue_pair<R>(s0, a, 0, q.x, q.pblk, q.lrow);
-    issue_pair<R>(s2, a, 2, q.x, q.pblk, q.lrow);
-    st[1] = rtc_stamp();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PairSpan<R>::NC) : "memory");
-    st[2] = rtc_stamp();
-    auto sink = [&](int ch, float v) {
-        if (q.active) q.outp[(long long)ch * a.HW] = v;
-    };
-    finish_pair<R>(s0, a, 0, q.x, q.pp, sink);
-    st[3] = rtc_stamp();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (2 * R + 1)) : "memory");
-    st[4] = rtc_stamp();
-    finish_pair<R>(s2, a, 2, q.x, q.pp, sink);
-    st[5] = rtc_stamp();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st[6] = rtc_stamp();
-    unsigned hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    if ((threadIdx.x & 63) == 0) {
-        unsigned long long *d = a.dbg + ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) d[k] = st[k];
-        d[7] = hw;
-    }
-}
-#endif
-
-template <int R>
-static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
-    const unsigned nblk = (unsigned)((a.P + 255) / 256);
-#ifdef RAFTCORR_DEV
-    if constexpr (R == 4) {
-        const int v = dev_knob("RAFTCORR_LOOKUP_VARIANT");
-        if ((a.levels == 4 || a.levels == 2) && !a.out_cl && v >= 212 && v <= 214) {
-            if (v == 212) launch_pair_coop<R, 1>(a, bf16, s);
-            if (v == 213) launch_pair_coop<R, 2>(a, bf16, s);
-            if (v == 214) launch_pair_coop<R, 4>(a, bf16, s);
-            return hipGetLastError();
-        }
-        // persistent pair lookup: 215 = one group at a time, 2 blocks/CU;
-        // 216 / 217 = pipelined, 1 / 2 blocks per CU (more spill to scratch)
-        if ((a.levels == 4 || a.levels == 2) && !a.out_cl && v >= 215 && v <= 217) {
-            if (v == 215) launch_pair_persist<R, false, 2>(a, bf16, 2, s);
-            if (v == 216) launch_pair_persist<R, true, 1>(a, bf16, 1, s);
-            if (v == 217) launch_pair_persist<R, true, 2>(a, bf16, 2, s);
-            return hipGetLastError();
-        }
-        // 220: level-0 chain (reads level 0 only; fp32, 4 levels)
-        if (a.levels == 4 && !bf16 && !a.out_cl && v == 220) {
-            hipLaunchKernelGGL((lookup_l0chain_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
-            return hipGetLastError();
-        }
-        if (a.levels == 4 && v == 210 && a.dbg) {
-            hipLaunchKernelGGL((lookup_pair_stamped_kernel<R>), dim3(nblk), dim3(256), 0, s, a);
-            return hipGetLastError();
-        }
-        if (a.levels == 4 && v >= 201 && v <= 211) {
-            if (v == 211 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 9>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 211 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 9, true>), dim3(nblk), dim3(256), 0, s, a);
-            // 208 / 209: at least 5 / 6 waves per SIMD (register cap)
-            if (v == 208 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 5>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 208 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 5>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 209 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 6>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 209 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 6>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 207 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 7>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 207 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 7, true>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 205 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 5>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 206 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 6>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 205 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 5, true>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 206 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 6, true>), dim3(nblk), dim3(256), 0, s, a);
-            // every variant in the pyramid's own element type (an fp32 kernel
-            // on a bf16 pyramid reads past the end of its buffers)
-            if (v == 201 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 202 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 201 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 202 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 2, true>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 203 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 204 && !bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 4>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 203 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 3, true>), dim3(nblk), dim3(256), 0, s, a);
-            if (v == 204 && bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 4, true>), dim3(nblk), dim3(256), 0, s, a);
-            return hipGetLastError();
-        }
-    }
-#endif
-    const bool cl = a.out_cl != 0;
-    if (a.levels == 4) {
-        if (cl) {
-            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-        } else {
-            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true>), dim3(nblk), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
-        }
-    } else if (a.levels == 2) {
-        if (cl) {
-            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, false, 1, true>), dim3(nblk), dim3(256), 0, s, a);
-        } else {
-            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true>), dim3(nblk), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
-        }
-    } else {
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template <int R, int M>
-static hipError_t launch_chain_m(const LookupArgs &a, hipStream_t s, unsigned lds = 0) {
-    const unsigned nblk = (unsigned)((a.P + 255) / 256);
-    if (a.levels == 4)
-        hipLaunchKernelGGL((lookup_chain_kernel<R, 4, M>), dim3(nblk), dim3(256), lds, s, a);
-    else if (a.levels == 3)
-        hipLaunchKernelGGL((lookup_chain_kernel<R, 3, M>), dim3(nblk), dim3(256), lds, s, a);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
-template <int R>
-static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
-#ifdef RAFTCORR_DEV
-    if constexpr (R == 4) {   // ablation variants (dev library), config-2 radius
-        const int variant = dev_knob("RAFTCORR_LOOKUP_VARIANT");
-        if (variant == 101) return launch_chain_m<R, 1>(a, s);
-        if (variant == 102) return launch_chain_m<R, 2>(a, s);
-        if (variant == 103) return launch_chain_m<R, 3>(a, s);
-        if (variant == 104) return launch_chain_m<R, 4>(a, s);
-        if (variant == 105) return launch_chain_m<R, 5>(a, s);   // non-temporal output stores
-    }
-#endif
-    return launch_chain_m<R, 0>(a, s);
-}
+// Below this many pixels the launch cannot fill the chip with the 256-thread
+// runtime-loop kernel (one dependent memory round trip per level): use
+// 64-thread blocks and issue every level's loads up front instead.
+constexpr long long kSmallP = 256LL * 256 * 2;
+// Below this many pixels one wave per (64 pixels, level) still leaves the
+// chip under-filled or about full: lookup_levelpar_kernel.
+constexpr long long kLevelParP = 64LL * 1024;
 
 // ---- lookup fused with the motion encoder's convc1 (+ ReLU) ----
 // BasicMotionEncoder.convc1 (model.py:199, :206) is a 1x1 conv over the
@@ -1429,15 +828,66 @@ __global__ __launch_bounds__(256) void lookup_conv_kernel(LookupArgs a, const fl
     }
 }
 
+template <int R, int M>
+static hipError_t launch_chain_m(const LookupArgs &a, hipStream_t s, unsigned lds = 0) {
+    const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    if (a.levels == 4)
+        hipLaunchKernelGGL((lookup_chain_kernel<R, 4, M>), dim3(nblk), dim3(256), lds, s, a);
+    else if (a.levels == 3)
+        hipLaunchKernelGGL((lookup_chain_kernel<R, 3, M>), dim3(nblk), dim3(256), lds, s, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+#ifdef RAFTCORR_DEV
+#include "dev/lookup_dev.inc"   // A/B variants and prototypes: libraftcorr_dev.so only
+#endif
+
+template <int R>
+static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
+    const unsigned nblk = (unsigned)((a.P + 255) / 256);
+#ifdef RAFTCORR_DEV
+    if (const hipError_t e = dev_launch_pair<R>(a, bf16, s); e != hipErrorNotSupported) return e;
+#endif
+    const bool cl = a.out_cl != 0;
+    if (a.levels == 4) {
+        if (cl) {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, false, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+        } else {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 4, 0, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+        }
+    } else if (a.levels == 2) {
+        if (cl) {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, false, 1, true>), dim3(nblk), dim3(256), 0, s, a);
+        } else {
+            if (bf16) hipLaunchKernelGGL((lookup_pair_kernel<R, 2, 0, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((lookup_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+        }
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int R>
+static hipError_t launch_chain_r(const LookupArgs &a, hipStream_t s) {
+#ifdef RAFTCORR_DEV
+    if (const hipError_t e = dev_launch_chain<R>(a, s); e != hipErrorNotSupported) return e;
+#endif
+    return launch_chain_m<R, 0>(a, s);
+}
+
 template <int R>
 static hipError_t launch_conv_r(const LookupArgs &a, int bf16, const float *w, const float *b,
                                 int cout, int relu, float *out, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
 #ifdef RAFTCORR_DEV
-    if (dev_knob("RAFTCORR_CONV_VARIANT") == 1 && a.levels == 4 && !bf16) {   // one level at a time
-        hipLaunchKernelGGL((lookup_conv_kernel<R, 4, false, false>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
-        return hipGetLastError();
-    }
+    if (const hipError_t e = dev_launch_conv<R>(a, bf16, w, b, cout, relu, out, s); e != hipErrorNotSupported)
+        return e;
 #endif
     if (a.levels == 4) {
         if (bf16) hipLaunchKernelGGL((lookup_conv_kernel<R, 4, true>), dim3(nblk), dim3(256), 0, s, a, w, b, cout, relu, out);
@@ -1454,34 +904,21 @@ static hipError_t launch_conv_r(const LookupArgs &a, int bf16, const float *w, c
     return hipGetLastError();
 }
 
-template <int R, int NL, bool BF16, bool EXACT, int BS = 256, int WPE = 1>
-static void launch_k(const LookupArgs &a, hipStream_t s) {
-    const unsigned nblk = (unsigned)((a.P + BS - 1) / BS);
-    hipLaunchKernelGGL((lookup_kernel<R, NL, BF16, EXACT, BS, WPE>), dim3(nblk), dim3(BS), 0, s, a);
-}
-
-// Below this many pixels the launch cannot fill the chip with the 256-thread
-// runtime-loop kernel (one dependent memory round trip per level): use
-// 64-thread blocks and issue every level's loads up front instead.
-constexpr long long kSmallP = 256LL * 256 * 2;
-// Below this many pixels one wave per (64 pixels, level) still leaves the
-// chip under-filled or about full: lookup_levelpar_kernel.
-constexpr long long kLevelParP = 64LL * 1024;
-
 template <int R>
-static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream_t s) {
+static hipError_t launch_r(const LookupArgs &a, int bf16, hipStream_t s) {
     // Default: runtime level loop (low VGPR count, 8 waves/SIMD) + exact-span
-    // predicated loads.  Variant 1: full windows; 3: levels unrolled (all
-    // loads first; ~130 VGPRs).  Measured (tools/ablate.py) before choosing.
-    const bool unroll = a.levels == 3 || a.levels == 4;
-#ifndef RAFTCORR_DEV
-    variant = 0;
+    // predicated loads; small problems: every level's loads up front (64-thread
+    // blocks) or one wave per level (lookup_levelpar_kernel).  Measured
+    // (tools/ablate.py) before choosing.
+#ifdef RAFTCORR_DEV
+    if (const hipError_t e = dev_launch_level<R>(a, bf16, s); e != hipErrorNotSupported) return e;
 #endif
-    if (variant == 0 && a.P < kLevelParP && a.levels <= 4) {
+    const bool unroll = a.levels == 3 || a.levels == 4;
+    if (a.P < kLevelParP && a.levels <= 4) {
         const unsigned nblk = (unsigned)((a.P + 63) / 64);
         if (bf16) hipLaunchKernelGGL((lookup_levelpar_kernel<R, true>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
         else hipLaunchKernelGGL((lookup_levelpar_kernel<R, false>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
-    } else if (variant == 0 && a.P < kSmallP && unroll) {
+    } else if (a.P < kSmallP && unroll) {
         if (a.levels == 4) {
             if (bf16) launch_k<R, 4, true, true, 64>(a, s);
             else launch_k<R, 4, false, true, 64>(a, s);
@@ -1489,21 +926,6 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
             if (bf16) launch_k<R, 3, true, true, 64>(a, s);
             else launch_k<R, 3, false, true, 64>(a, s);
         }
-#ifdef RAFTCORR_DEV
-    } else if (variant == 6 && a.P < kLevelParP && a.levels <= 4) {   // blocks in launch order
-        const unsigned nblk = (unsigned)((a.P + 63) / 64);
-        if (bf16) hipLaunchKernelGGL((lookup_levelpar_kernel<R, true, false>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
-        else hipLaunchKernelGGL((lookup_levelpar_kernel<R, false, false>), dim3(nblk), dim3(64 * a.levels), 0, s, a);
-    } else if (variant == 1) {
-        if (bf16) launch_k<R, 0, true, false>(a, s);
-        else launch_k<R, 0, false, false>(a, s);
-    } else if (variant == 4 && a.levels == 4) {
-        if (bf16) launch_k<R, 4, true, true, 256, 4>(a, s);
-        else launch_k<R, 4, false, true, 256, 4>(a, s);
-    } else if (variant == 3 && a.levels == 4) {
-        if (bf16) launch_k<R, 4, true, true>(a, s);
-        else launch_k<R, 4, false, true>(a, s);
-#endif
     } else {
         if (bf16) launch_k<R, 0, true, true>(a, s);
         else launch_k<R, 0, false, true>(a, s);
@@ -1513,50 +935,20 @@ static hipError_t launch_r(const LookupArgs &a, int bf16, int variant, hipStream
 
 }  // namespace rc
 
-// RAFTCORR_LOOKUP_VARIANT (dev library only, read per call): see launch_r.
 hipError_t rc_launch_lookup(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;
-#ifdef RAFTCORR_DEV
-    const int variant = rc::dev_knob("RAFTCORR_LOOKUP_VARIANT");
-#else
-    const int variant = 0;
-#endif
     switch (radius) {
-        case 1: return rc::launch_r<1>(a, pyr_bf16, variant, s);
-        case 2: return rc::launch_r<2>(a, pyr_bf16, variant, s);
-        case 3: return rc::launch_r<3>(a, pyr_bf16, variant, s);
-        case 4: return rc::launch_r<4>(a, pyr_bf16, variant, s);
-        case 5: return rc::launch_r<5>(a, pyr_bf16, variant, s);
-        case 6: return rc::launch_r<6>(a, pyr_bf16, variant, s);
-        case 7: return rc::launch_r<7>(a, pyr_bf16, variant, s);
-        case 8: return rc::launch_r<8>(a, pyr_bf16, variant, s);
+        case 1: return rc::launch_r<1>(a, pyr_bf16, s);
+        case 2: return rc::launch_r<2>(a, pyr_bf16, s);
+        case 3: return rc::launch_r<3>(a, pyr_bf16, s);
+        case 4: return rc::launch_r<4>(a, pyr_bf16, s);
+        case 5: return rc::launch_r<5>(a, pyr_bf16, s);
+        case 6: return rc::launch_r<6>(a, pyr_bf16, s);
+        case 7: return rc::launch_r<7>(a, pyr_bf16, s);
+        case 8: return rc::launch_r<8>(a, pyr_bf16, s);
         default: return hipErrorInvalidValue;
     }
 }
-
-#ifdef RAFTCORR_DEV
-// Dev-only entry: the sheared pair lookup (fp32, 4 levels, r = 4) over levels
-// 0 and 2 stored as S_i[b,h][k][w1] (K0 / K2 rows of ldw floats per image row).
-extern "C" int rc_dev_lookup_sheared_pair(const void *lvl0, const void *lvl2, long K0, long K2, long ldw,
-                                          const int *widths, const float *coords_x, long cbs, int B, int H,
-                                          int W1, float *out, void *stream) {
-    rc::LookupArgs a{};
-    for (int i = 0; i < 4; ++i) a.W[i] = widths[i];
-    a.coords = coords_x;
-    a.cbs = cbs;
-    a.out = out;
-    a.P = (long long)B * H * W1;
-    a.HW = H * W1;
-    a.W1 = W1;
-    a.levels = 4;
-    if (a.P <= 0) return 0;
-    const unsigned nblk = (unsigned)((a.P + 255) / 256);
-    hipLaunchKernelGGL((rc::lookup_sheared_pair_kernel<4>), dim3(nblk), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), a, static_cast<const float *>(lvl0),
-                       static_cast<const float *>(lvl2), (long long)K0, (long long)K2, (long long)ldw);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
-}
-#endif
 
 hipError_t rc_launch_lookup_pair(const rc::LookupArgs &a, int radius, int pyr_bf16, hipStream_t s) {
     if (a.P <= 0) return hipSuccess;

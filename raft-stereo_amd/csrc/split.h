@@ -66,17 +66,4 @@ __device__ __forceinline__ void sp_mma6(f32x4 &c, const SplitFrag &x, const Spli
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.h, y.h, c, 0, 0, 0);
 }
 
-// The same six products on v_mfma_f32_32x32x16_bf16 (32 cycles per SIMD, of
-// which it holds the vector issue for 8: three times the room for the split's
-// VALU per MFMA cycle of the 16x16x32 form, whose 16 cycles hold it for 8).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ void sp_mma6_32(f32x16 &c, const SplitFrag &x, const SplitFrag &y) {
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.m, y.m, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.h, y.l, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.l, y.h, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.h, y.m, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.m, y.h, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x.h, y.h, c, 0, 0, 0);
-}
-
 }  // namespace rc

@@ -1,6 +1,5 @@
-// Pieces shared by the split-bf16 volume kernels (volume_split.hip: the
-// 4-wave kernel; volume_split8.hip: the 8-wave kernel): the LDS-DMA ring's
-// geometry and a lane's fragment read + split.
+// Pieces of the split-bf16 volume kernel (volume_split.hip): the LDS-DMA
+// ring's geometry and a lane's fragment read + split.
 #pragma once
 #include "common.h"
 #include "epilogue.h"

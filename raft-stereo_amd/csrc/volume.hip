@@ -1026,15 +1026,6 @@ static void launch_bf16_ring_n(const BuildArgs &a, hipStream_t s, int per_cu = 1
                            dim3(128 * NWN + 128), 0, s, a, (int)ntiles, tiles_m, tiles_n);
 }
 
-#ifdef RAFTCORR_DEV
-// dev: the 6-wave shape (128-wide w2 tiles, 75 / 65 KB of LDS) resident
-// twice per CU, so two independent barrier chains share each CU
-template <int MODE>
-static void launch_bf16_ring_two(const BuildArgs &a, bool defer, int per_cu, hipStream_t s) {
-    if (defer) launch_bf16_ring_n<2, 4, 4, MODE, true>(a, s, per_cu);
-    else launch_bf16_ring_n<2, 4, 3, MODE, false>(a, s, per_cu);
-}
-#endif
 
 // the deferred-epilogue kernel has no staging area: 4 ring slots
 template <int MODE>
@@ -1217,15 +1208,14 @@ static void launch_ring(const BuildArgs &a, hipStream_t s) {
     hipLaunchKernelGGL((build_f32_ring_kernel<4, MODE, SL>), dim3((unsigned)nwg), dim3(256), 0, s, a, (int)nwg);
 }
 
+#ifdef RAFTCORR_DEV
+#include "dev/volume_dev.inc"   // ablation modes and measured variants: libraftcorr_dev.so only
+#endif
+
 template <bool IN_BF16, bool ALIGNED>
 static void launch_bf16(const BuildArgs &a, unsigned nwg, hipStream_t s) {
 #ifdef RAFTCORR_DEV
-    switch (dev_knob("RAFTCORR_BUILD_MODE")) {   // dev-only ablation (see rc_launch_build_f32)
-        case 1: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 1>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); return;
-        case 2: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 2>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); return;
-        case 3: hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 3>), dim3(nwg), dim3(256), 0, s, a, (int)nwg); return;
-        default: break;
-    }
+    if (dev_launch_bf16_pw<IN_BF16, ALIGNED>(a, nwg, s)) return;
 #endif
     hipLaunchKernelGGL((build_bf16_kernel<IN_BF16, ALIGNED, 0>), dim3(nwg), dim3(256), 0, s, a, (int)nwg);
 }
@@ -1241,40 +1231,7 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
     const unsigned n = (unsigned)nwg;
     rc::B16Shape sh = in_bf16 ? rc::bf16_ring_shape(a) : rc::B16Shape{0, 0, false};
 #ifdef RAFTCORR_DEV
-    // 32: per-wave kernel; ring ablations (timing only, all without epilogue
-    // stores): 40 product, 41 no DMA, 44 no fragment reads / MFMA, 45
-    // neither, 48 16-B-aligned (wrong) DMA sources
-    const int mode = rc::dev_knob("RAFTCORR_BUILD_MODE");
-    if (mode == 32) sh = rc::B16Shape{0, 0, false};
-    if (sh.nwn && (mode == 52 || mode == 53)) {   // stores spread over 8 stages / staggered by wave parity
-        if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
-        if (mode == 52) rc::launch_bf16_ring<rc::kModeSpread>(a, sh, s);
-        else rc::launch_bf16_ring<rc::kModeStagger>(a, sh, s);
-        return hipGetLastError();
-    }
-    if (sh.nwn && (mode == 49 || mode == 50 || mode == 51)) {   // 6-wave shape: 2 / 1 per CU; 51: 2, no stores
-        if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
-        if (mode == 51) rc::launch_bf16_ring_two<2>(a, sh.defer, 2, s);
-        else rc::launch_bf16_ring_two<0>(a, sh.defer, mode == 49 ? 2 : 1, s);
-        return hipGetLastError();
-    }
-    if (sh.nwn && mode >= 40 && mode <= 55 && mode != 49 && mode != 50 && mode != 51 && mode != 52 && mode != 53) {
-        if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
-        switch (mode) {
-            case 40: rc::launch_bf16_ring<2>(a, sh, s); break;
-            case 41: rc::launch_bf16_ring<3>(a, sh, s); break;
-            case 44: rc::launch_bf16_ring<6>(a, sh, s); break;
-            case 45: rc::launch_bf16_ring<7>(a, sh, s); break;
-            case 42: rc::launch_bf16_ring<18>(a, sh, s); break;   // no stores, MFMA without fragment reads
-            case 43: rc::launch_bf16_ring<19>(a, sh, s); break;   // ... and no DMA
-            case 46: rc::launch_bf16_ring<1>(a, sh, s); break;   // no DMA, with stores
-            case 47: rc::launch_bf16_ring<5>(a, sh, s); break;   // no DMA, no MFMA, with stores
-            case 54: rc::launch_bf16_ring<rc::kModeL2Stores | 5>(a, sh, s); break;   // 47 with L2-resident stores
-            case 55: rc::launch_bf16_ring<rc::kModeL2Stores>(a, sh, s); break;       // product, L2-resident stores
-            default: rc::launch_bf16_ring<10>(a, sh, s); break;
-        }
-        return hipGetLastError();
-    }
+    if (const hipError_t e = rc::dev_launch_bf16mma(a, sh, s); e != hipErrorNotSupported) return e;
 #endif
     if (sh.nwn) {
         if (a.nfused > rc::kB16MaxFused) a.nfused = rc::kB16MaxFused;
@@ -1291,10 +1248,7 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
     return hipGetLastError();
 }
 
-// RAFTCORR_BUILD_MODE (dev library only, read per call): 0 = product (LDS-DMA
-// ring kernel, 3 slots), 2 = ring without epilogue stores, 4 / 5 = 4- / 5-slot
-// ring; 128+flags = the direct-load
-// kernel (flags 1 no operand loads, 2 no stores, 64 stagger).
+// The exact fp32 MFMA build (LDS-DMA ring kernel, 3 slots).
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
     const long long nwg = (long long)a.B * a.H * a.tiles_m * a.tiles_n;
     if (nwg <= 0) return hipSuccess;
@@ -1306,17 +1260,7 @@ hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s) {
         return hipGetLastError();
     }
 #ifdef RAFTCORR_DEV
-    switch (rc::dev_knob("RAFTCORR_BUILD_MODE")) {
-        case 2: rc::launch_ring<2>(a, s); return hipGetLastError();
-        case 4: rc::launch_ring<0, 4>(a, s); return hipGetLastError();         // 4-slot ring
-        case 5: rc::launch_ring<0, 5>(a, s); return hipGetLastError();         // 5-slot ring
-        case 128: rc::launch<true, 2, 0>(a, n, s); return hipGetLastError();   // direct-load kernel
-        case 130: rc::launch<true, 2, 2>(a, n, s); return hipGetLastError();
-        case 131: rc::launch<true, 2, 3>(a, n, s); return hipGetLastError();
-        case 129: rc::launch<true, 2, 1>(a, n, s); return hipGetLastError();
-        case 192: rc::launch<true, 2, 64>(a, n, s); return hipGetLastError();
-        default: break;
-    }
+    if (const hipError_t e = rc::dev_launch_f32(a, n, s); e != hipErrorNotSupported) return e;
 #endif
     rc::launch_ring<0>(a, s);
     return hipGetLastError();

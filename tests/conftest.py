@@ -33,3 +33,31 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+class _DevLibraryOrSkip:
+    """``_lib.dev_library()`` for the variant bit-identity tests: the dev
+    library (libraftcorr_dev.so: A/B knobs, ablation variants) is not pushed
+    to the GPU box by default (.gpurunignore), so a test that needs it skips
+    when it is absent instead of failing; the product library never needs it."""
+
+    def __init__(self):
+        from raft_stereo_amd import _lib
+        self._inner = _lib._DevLibrary()
+
+    def __enter__(self):
+        from raft_stereo_amd import _lib
+        if not os.path.exists(_lib.DEV_LIB_PATH):
+            pytest.skip("libraftcorr_dev.so not present (dev-library variant test)")
+        return self._inner.__enter__()
+
+    def __exit__(self, *exc):
+        return self._inner.__exit__(*exc)
+
+
+def _install_dev_library_skip():
+    from raft_stereo_amd import _lib
+    _lib.dev_library = _DevLibraryOrSkip
+
+
+_install_dev_library_skip()

@@ -47,38 +47,27 @@ def main():
     B, D, H, W1, W2, L, r, iters, _ = cfg
     dev = torch.device("cuda", 0)
     ll = a.config in bench.LOW_LATENCY_CONFIGS
-    # "K/M": the split kernel K (RAFTCORR_SPLIT_KERNEL: 8 = the 8-wave kernel)
-    # under mode M; a plain integer M: the 4-wave kernel
-    variants = ["exact", "ws"] + [m if "/" in m else int(m) for m in a.modes.split(",") if m]
+    # RAFTCORR_SPLIT_MODE values of the split kernel (dev library)
+    variants = ["exact"] + [int(m) for m in a.modes.split(",") if m]
     res = {str(v): [] for v in variants}
     with torch.no_grad():
         f1, f2, _ = bench.make_inputs(cfg, dev, seed=1)
 
         def run(v):
-            os.environ["RAFTCORR_SPLIT_KERNEL"] = "0"
             if v == "exact":
                 os.environ["RAFTCORR_SPLIT_MODE"] = "0"
                 return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll, exact_f32=True)
-            if v == "ws":           # the warp-specialised kernel (dev only, not kept)
-                os.environ["RAFTCORR_SPLIT_MODE"] = "0"
-                os.environ["RAFTCORR_SPLIT_KERNEL"] = "3"
-                return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
-            if isinstance(v, str):                   # "K/M"
-                kk, mm = v.split("/")
-                os.environ["RAFTCORR_SPLIT_KERNEL"] = kk
-                os.environ["RAFTCORR_SPLIT_MODE"] = mm
-            else:
-                os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
+            os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
             return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
         ref = None
         for v in variants:
             blk = run(v)()
             if v == 0:
                 ref = [t.clone() for t in blk.corr_pyramid[:4]]
-        # schedule variants (128 / 256) must reproduce the product bit for bit
+        # variants with math and stores (no 1/2/4 ablation bits) must
+        # reproduce the product bit for bit
         for v in variants:
-            checked = isinstance(v, str) and "/" in v and not (int(v.split("/")[1]) & 7)   # "K/M", math + stores
-            if (checked or (isinstance(v, int) and v >= 128)) and ref is not None:
+            if isinstance(v, int) and v and not (v & 7) and ref is not None:
                 got = run(v)().corr_pyramid[:4]
                 res.setdefault("bit_identical", {})[str(v)] = all(
                     bool(torch.equal(x, y)) for x, y in zip(got, ref))
@@ -89,7 +78,6 @@ def main():
                 fn = run(v)
                 res[str(v)] += time_launches(fn, a.per)
         os.environ["RAFTCORR_SPLIT_MODE"] = "0"
-        os.environ["RAFTCORR_SPLIT_KERNEL"] = "0"
     ident = res.pop("bit_identical", {})
     nerr = res.pop("norm_err_vs_0", {})
     out = {k: {"median_us": statistics.median(x), "min_us": min(x)} for k, x in res.items()}
@@ -100,9 +88,9 @@ def main():
     for k, v in out.items():
         v["fp32_equiv_tflops"] = flops / (v["median_us"] * 1e-6) / 1e12
     print(json.dumps({"config": a.config, "variants": out,
-                      "legend": "exact = fp32 MFMA ring; ws = warp-specialised split kernel (not kept); split "
-                                "modes (build_split_kernel): 0 product, 1 no loads, 2 no stores, "
-                                "4 no MFMA (sums combine)"}, indent=1))
+                      "legend": "exact = fp32 MFMA ring; split modes (build_split_kernel): 0 "
+                                "product, 1 no loads, 2 no stores, 4 no MFMA, 4096 no wave-role "
+                                "rotation (sums combine)"}, indent=1))
 
 
 if __name__ == "__main__":

@@ -23,6 +23,7 @@ step() {  # step <name> <timeout> cmd...
     return 0
 }
 rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
+has tsplit && step pytest_split 600 python -u -m pytest tests/test_split_gpu.py tests/test_configs_gpu.py -v -rf --timeout 120 --timeout-method thread
 has test  && step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has bench && step bench 600 python bench.py
@@ -30,7 +31,6 @@ has e2e && step e2e_probe 900 python tools/e2e_probe.py
 has probe && step line_probe 300 python tools/line_probe.py
 has lprobe && step lookup_probe 300 python tools/lookup_probe.py --dev-variants ${LPROBE_VARIANTS:-201,202}
 has gprobe && step gather_probe 300 python tools/gather_probe.py
-has timeline && step lookup_timeline 300 python tools/lookup_timeline.py
 has shard && step shard_probe 600 python tools/shard_probe.py
 has ablate && step ablate 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --chain
 has ablateb && step ablate_bwd 600 python tools/ablate.py --build-modes 0 --lookup-variants 0 --bwd
@@ -131,7 +131,11 @@ if has shadowk; then   # config-3 shadow copies re-decided as
         done
     done
 fi
+has rtab && step realtime_ab 300 python tools/realtime_ab.py ${RTAB_VARIANTS:-RAFTCORR_LOOKUP_VARIANT=6}
+has rtg && step bench_realtime_graph 300 python bench.py --config realtime --graph --no-cpu-baseline --steps 200 --warmup 10
 has shard8 && step shard_probe_h8 900 python tools/shard_probe.py --halo 8
+has sablr && step build_ablate_realtime 300 python tools/build_ablate.py --config realtime --modes ${SABL_MODES:-0,4096} --rounds 9
+has sablm && step build_ablate_middlebury 300 python tools/build_ablate.py --config middlebury --modes ${SABL_MODES:-0,4096} --rounds 5
 has sabl && step build_ablate 600 python tools/build_ablate.py --modes ${SABL_MODES:-0,8192} --rounds ${SABL_ROUNDS:-9} ${SABL_CONFIG:+--config $SABL_CONFIG}
 has shear && step shear_probe 600 python tools/shear_probe.py
 has gfloor && step graph_floor 300 python tools/graph_floor.py
