@@ -121,6 +121,17 @@ has launch && step launch_gloo2 600 env RAFTCORR_BENCH_BACKEND=gloo python bench
 has netmb && step net_middlebury_1 600 python bench.py --config middlebury --network --steps 2 --warmup 1 --no-cpu-baseline
 has netmb && step net_middlebury_gloo2 900 env RAFTCORR_BENCH_BACKEND=gloo python bench.py --gpus 2 --config middlebury --network --steps 1 --warmup 1 --no-cpu-baseline
 has pconv && step shard_probe_perconv 900 python tools/shard_probe.py --perconv
+if has shadows; then   # config 2 / 4: level-0 shadow copy and NHWC output re-measured as whole steps
+    BQ="--no-cpu-baseline --e2e-steps 0 --no-backward --config4-steps 0 --steps 20 --warmup 5"
+    for rep in 1 2; do
+        step shadows_sf_default_$rep 300 python bench.py $BQ
+        step shadows_sf_02_$rep 300 python bench.py $BQ --shadow 0,2
+        step shadows_sf_cl_$rep 300 python bench.py $BQ --channels-last
+        step shadows_sf_02cl_$rep 300 python bench.py $BQ --shadow 0,2 --channels-last
+        step shadows_mb_default_$rep 300 python bench.py --config middlebury $BQ
+        step shadows_mb_02_$rep 300 python bench.py --config middlebury $BQ --shadow 0,2
+    done
+fi
 if has shadowk; then   # config-3 shadow copies re-decided as whole steps
     for rep in 1 2; do
         for SH in default 2 none; do
