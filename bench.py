@@ -89,7 +89,15 @@ GLOBAL_BATCH_CONFIGS = {"kitti"}
 LOW_LATENCY_CONFIGS = {"realtime"}
 
 
-def make_inputs(cfg, device, seed, dtype=torch.float32):
+FIELDS = ("random", "smooth", "slant")
+
+
+def make_inputs(cfg, device, seed, dtype=torch.float32, field="random"):
+    """randn fmaps and one coords tensor per iteration.  ``field``: the
+    disparity d of x = w1 - d -- "random" U[0, 64) per pixel, a fresh draw per
+    iteration (the headline); "smooth" a bilinear field from a
+    9x16 grid of U[0, 64) with +-0.25 px of noise; "slant" planes with
+    |slope| <= 0.25 px/px -- the coherent fields a network's coords resemble."""
     B, D, H, W1, W2, L, r, iters, _ = cfg
     g = torch.Generator().manual_seed(seed)
     f1 = torch.randn(B, D, H, W1, generator=g).to(device, dtype)
@@ -99,7 +107,22 @@ def make_inputs(cfg, device, seed, dtype=torch.float32):
     for it in range(iters):
         gi = torch.Generator().manual_seed(seed * 1000 + it + 1)
         c = grid.clone()
-        c[:, 0] -= torch.rand(B, H, W1, generator=gi) * 64.0
+        if field == "random":
+            d = torch.rand(B, H, W1, generator=gi) * 64.0
+        elif field == "smooth":
+            k = torch.rand(B, 1, 9, 16, generator=gi) * 64.0
+            d = torch.nn.functional.interpolate(k, size=(H, W1), mode="bilinear", align_corners=True)[:, 0]
+            d = d + (torch.rand(B, H, W1, generator=gi) - 0.5) * 0.5
+        elif field == "slant":
+            a0 = torch.rand(B, 1, 1, generator=gi) * 32 + 16
+            bw = (torch.rand(B, 1, 1, generator=gi) - 0.5) * 0.5
+            ch = (torch.rand(B, 1, 1, generator=gi) - 0.5) * 0.5
+            w = torch.arange(W1).view(1, 1, W1) - W1 / 2
+            h = torch.arange(H).view(1, H, 1) - H / 2
+            d = (a0 + bw * w + ch * h).clamp(0, 63.9) + torch.rand(B, H, W1, generator=gi) * 0.25
+        else:
+            raise ValueError(f"unknown coords field {field!r}")
+        c[:, 0] -= d
         coords.append(c.to(device))
     return f1, f2, coords
 
@@ -540,6 +563,11 @@ def main():
     ap.add_argument("--shadow", default="default",
                     help="pyramid levels with an RC_SHADOW copy: 'default' (per-shape rule, "
                          "corr.default_shadow_levels), 'none', or a comma list such as 0,2")
+    ap.add_argument("--layout", default="rows", choices=("rows", "disparity"),
+                    help="CorrBlock1D pyramid layout: the reference's rows (default) or the opt-in "
+                         "disparity-major levels (RC_LAYOUT_DISPARITY, DESIGN.md §3.2h)")
+    ap.add_argument("--field", default="random", choices=FIELDS,
+                    help="coords field: random (SURVEY §8d, the headline), smooth or slant (coherent)")
     ap.add_argument("--network", action="store_true",
                     help="--config middlebury: the line's value is the row-sharded FULL network "
                          "(BASELINE configs[3]: 1984x2880, 32 iterations, GRU halo exchange) "
@@ -602,14 +630,14 @@ def main():
         # (strong scaling); the corr path is row-local, so no exchange.
         from raft_stereo_amd.shard import split_range
         r0, r1 = split_range(H, rank, split_world)
-        f1, f2, coords = make_inputs(cfg, device, seed=1)
+        f1, f2, coords = make_inputs(cfg, device, seed=1, field=args.field)
         f1 = f1[:, :, r0:r1].contiguous()
         f2 = f2[:, :, r0:r1].contiguous()
         coords = [c[:, :, r0:r1].contiguous() for c in coords]
         H = r1 - r0
     else:
         f1, f2, coords = make_inputs(cfg, device, seed=1 + rank,
-                                     dtype=torch.bfloat16 if bf16 else torch.float32)
+                                     dtype=torch.bfloat16 if bf16 else torch.float32, field=args.field)
     P = B * H * W1
 
     def step(ev=None):
@@ -617,7 +645,7 @@ def main():
             ev[0].record()
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
                           low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32,
-                          shadow=shadow)
+                          shadow=shadow, layout=args.layout)
         if ev is not None:
             ev[1].record()
         for it in range(iters):
@@ -686,7 +714,7 @@ def main():
             e0.record()
             CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
                         low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32,
-                        shadow=shadow)
+                        shadow=shadow, layout=args.layout)
             e1.record()
             torch.cuda.synchronize()
             bl.append(e0.elapsed_time(e1))
@@ -699,7 +727,7 @@ def main():
         # passes of all launches.
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=args.channels_last,
                           low_latency=args.config in LOW_LATENCY_CONFIGS, exact_f32=args.exact_f32,
-                          shadow=shadow)
+                          shadow=shadow, layout=args.layout)
         per_launch = []
         for _ in range(3):
             le = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
@@ -781,7 +809,8 @@ def main():
         roof_volume["mfma_util_pmc"] = vpmc["mfma_util"]
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     pair = blk._chain and (L == 2 or (L == 4 and 2 in written))
-    lfamily = ("rc::lookup_pair_kernel" if pair else "rc::lookup_chain_kernel" if blk._chain
+    lfamily = ("rc::lookup_sheared_pair_kernel" if args.layout == "disparity"
+               else "rc::lookup_pair_kernel" if pair else "rc::lookup_chain_kernel" if blk._chain
                else "rc::lookup_levelpar_kernel" if P < 65536 and L <= 4 else "rc::lookup_kernel")
     lname, lpmc = pmc_entry(pmc, lfamily)
     ltraffic = lpmc.get("hbm_bytes")
@@ -819,13 +848,15 @@ def main():
         "scaling": "strong" if ((row_shard or global_batch) and not proj) else "weak",
         "vs_baseline": None,
         "dtype": "bf16" if bf16 else "f32",
-        "data": "synthetic (randn fmaps, coords_grid - U[0,64) per iteration)",
+        "data": ("synthetic (randn fmaps, coords_grid - U[0,64) per iteration)" if args.field == "random"
+                 else f"synthetic (randn fmaps, coords_grid - a {args.field} disparity field in [0,64))"),
         "config": {"workload": desc + (" (HIP graph replay)" if args.graph else "")
                    + (f" (rows sharded over {world} ranks)" if row_shard else ""),
                    "config": args.config, "global_batch": run_pairs,
                    "fmap": [B, D, H, W1], "W2": W2, "levels": L, "radius": r, "iters": iters,
                    "parallelism": (f"row-shard x{world}" if row_shard else f"batch-shard x{world}"),
-                   "corr_out_layout": "channels_last" if args.channels_last else "nchw"},
+                   "corr_out_layout": "channels_last" if args.channels_last else "nchw",
+                   "pyramid_layout": args.layout, "coords_field": args.field},
         "roofline": dominant,
         "roofline_volume": roof_volume,
         "roofline_lookup": roof_lookup,
@@ -835,7 +866,11 @@ def main():
                       "lookup_in_loop": lookup_ms,
                       "lookup_per_launch": lookup_launch_ms},
         "cpu_baseline": None,
-        "notes": (f"pool-chain block: the build writes pyramid levels {written} (levels "
+        "notes": (f"disparity-major block (layout='disparity', RC_LAYOUT_DISPARITY): the build writes "
+                  f"levels {written} as S[b,h][k][w1], k = (w1 >> l) - j + W_l - 1 (the same values and "
+                  "bytes as the rows), the lookup reads them with the disparity-major pair kernel; "
+                  "corr_pyramid is gathered into rows only when read" if args.layout == "disparity" else
+                  f"pool-chain block: the build writes pyramid levels {written} (levels "
                   f"{sorted(blk._shadow)} also as a half-line-shifted RC_SHADOW copy: those "
                   "writes are in the build's time, not in its algorithmic bytes); every lookup "
                   "recomputes the others from them bit-exactly (rc_corr_lookup_chain); the rest "

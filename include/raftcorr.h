@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 8
+#define RC_ABI_VERSION 9
 
 /* element types */
 #define RC_F32  0
@@ -80,6 +80,26 @@ extern "C" {
  * the exception: an inf operand gives NaN in its row's volume where the fp32
  * GEMM gives +-inf; pass this flag for such inputs.  Ignored by bf16 builds. */
 #define RC_BUILD_EXACT_F32 0x20000
+
+/* Flag OR-ed into the pyr_dtype of rc_corr_build and rc_corr_lookup_chain
+ * (ABI v9): the pair layout's stored levels -- level 0, and level 2 of a
+ * 4-level pyramid (pyr[1] == NULL) -- are DISPARITY-MAJOR.  Level l of row
+ * block r = b*H + h is an array S of RC_SHEAR_ROWS(W2, W1, l) rows of
+ * pyr_ld[l] fp32 elements (pyr_ld[l] >= W1, a multiple of 4), at
+ * pyr[l] + r * RC_SHEAR_ROWS(W2, W1, l) * pyr_ld[l], with
+ *     S[k][w1] = C_l[(r, w1)][j],   k = (w1 >> l) - j + (W2 >> l) - 1,
+ * so the pixels of an image row that look at the same disparity read one
+ * contiguous run of a row of S.  Entries with j outside [0, W2 >> l) are
+ * neither written nor read.  The values are the row layout's bit for bit and
+ * so are the lookups (rc_corr_lookup_chain with the flag: the pair kernel's
+ * arithmetic); it pays where neighbouring pixels' coords agree (the
+ * network's fields), and loses on independent random coords (DESIGN.md
+ * §3.2h).  Requires fp32 fmaps and pyramid on the split-bf16 build (W1, W2
+ * multiples of 4, no RC_BUILD_EXACT_F32, no shadow copies), nbuf 1 (2 levels)
+ * or 3 with pyr[1] == NULL (4 levels), radius 1..4, NCHW output, each level
+ * under 4 GiB; RC_EUNSUPPORTED otherwise.  The other entry points refuse it. */
+#define RC_LAYOUT_DISPARITY 0x80000
+#define RC_SHEAR_ROWS(W2, W1, l) (((W2) >> (l)) + (((W1) - 1) >> (l)))
 
 /* return codes */
 #define RC_OK            0

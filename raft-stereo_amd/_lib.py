@@ -17,11 +17,17 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 RC_F32, RC_BF16 = 0, 1
 RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
-ABI_VERSION = 8
+ABI_VERSION = 9
 RC_SHADOW = 0xFF00  # pyr_dtype flags: every stored level carries a line-phase shadow copy
 RC_OUT_CHANNELS_LAST = 0x10000   # pyr_dtype flag: NHWC lookup output (pair kernel)
 RC_BUILD_EXACT_F32 = 0x20000     # rc_corr_build flag: exact fp32 MFMA kernel instead of the split-bf16 one
 RC_GRAD_OVERWRITE = 0x40000      # rc_corr_lookup_backward_calls flag: write the sum, do not add
+RC_LAYOUT_DISPARITY = 0x80000    # rc_corr_build / rc_corr_lookup_chain: disparity-major levels 0, 2 (ABI v9)
+
+
+def shear_rows(W2, W1, l):
+    """RC_SHEAR_ROWS: rows (diagonals) per image row of disparity-major level l."""
+    return (W2 >> l) + ((W1 - 1) >> l)
 
 
 def shadow_level(l):

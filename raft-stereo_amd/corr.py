@@ -341,6 +341,104 @@ def lookup_chain(pyramid, coords, num_levels, radius, shadow=False, channels_las
     return out
 
 
+# ------------------------------------------------- disparity-major layout
+# RC_LAYOUT_DISPARITY (ABI v9): the pair layout's stored
+# levels (0, and 2 of 4) as S_l[b,h][k][w1], k = (w1 >> l) - j + (W2 >> l) - 1.
+
+def _shear_ld(W1):
+    return -(-W1 // 4) * 4
+
+
+def shear_supported(fmap1, fmap2, num_levels, radius, pyramid_dtype):
+    """Why CorrBlock1D(layout="disparity") cannot serve these inputs, or None."""
+    if pyramid_dtype != torch.float32 or fmap1.dtype != torch.float32 or fmap2.dtype != torch.float32:
+        return "fp32 fmaps and an fp32 pyramid only"
+    if num_levels not in (2, 4) or not 1 <= radius <= 4:
+        return "the pair layout: 2 or 4 levels, radius 1..4"
+    B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+    if W1 % 4 or W2 % 4:
+        return "W1 and W2 multiples of 4 (the split-bf16 build)"
+    if W2 > 65536:
+        return "level-0 width <= 65536"
+    ld = _shear_ld(W1)
+    for l in ((0, 2) if num_levels == 4 else (0,)):
+        if B * H * _lib.shear_rows(W2, W1, l) * ld * 4 >= 0xFFFFFF00:
+            return f"disparity-major level {l} under 4 GiB"
+    return None
+
+
+def build_sheared(fmap1, fmap2, num_levels, exact_f32=False):
+    """rc_corr_build with RC_LAYOUT_DISPARITY: {0: S_0, 2: S_2 (4 levels)},
+    each a flat fp32 tensor of B*H*RC_SHEAR_ROWS rows of _shear_ld(W1)."""
+    if exact_f32:
+        raise ValueError("CorrBlock1D(layout='disparity') is built by the split-bf16 kernel only")
+    B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+    f1, f2 = _prep_fmap(fmap1), _prep_fmap(fmap2)
+    ld = _shear_ld(W1)
+    keep = (0, 2) if num_levels == 4 else (0,)
+    sh = {l: torch.empty(B * H * _lib.shear_rows(W2, W1, l) * ld, dtype=torch.float32, device=f1.device)
+          for l in keep}
+    if B * H * W1 == 0:
+        return sh
+    nbuf = 3 if num_levels == 4 else 1
+    ptrs = [sh[0].data_ptr(), None, sh[2].data_ptr()] if nbuf == 3 else [sh[0].data_ptr()]
+    lds = [ld, W2 >> 1, ld][:nbuf]
+    with torch.cuda.device(f1.device):
+        rc = _lib.lib().rc_corr_build(
+            f1.data_ptr(), f2.data_ptr(), _lib.RC_F32, B, D, H, W1, W2, _lib.ptr_array(ptrs),
+            _lib.long_array(lds), nbuf, _lib.RC_F32 | _lib.RC_LAYOUT_DISPARITY, _stream(f1.device))
+    _lib.check(rc, "rc_corr_build")
+    return sh
+
+
+def unshear_level(S, l, B, H, W1, W2):
+    """A disparity-major level as the reference's (B*H*W1, 1, 1, W2 >> l)
+    rows (row-padded buffer): the same values, gathered."""
+    W = W2 >> l
+    K = _lib.shear_rows(W2, W1, l)
+    ld = _shear_ld(W1)
+    w1 = torch.arange(W1, device=S.device)
+    kk = (w1 >> l)[:, None] - torch.arange(W, device=S.device)[None, :] + W - 1
+    rows = S.view(B * H, K, ld)[:, kk, w1[:, None].expand(W1, W)]
+    out = _level_buffer(B * H * W1, W, torch.float32, S.device, True)
+    out.copy_(rows.reshape(B * H * W1, 1, 1, W))
+    return out
+
+
+def lookup_sheared(sheared, coords, num_levels, radius, W2):
+    """rc_corr_lookup_chain with RC_LAYOUT_DISPARITY: the pair kernel's
+    results (bit for bit) from the disparity-major levels."""
+    _require_hip(coords, "coords")
+    if coords.dim() != 4 or coords.shape[1] < 1:
+        raise RuntimeError("CorrBlock1D: coords must be (B, 2, H, W1)")
+    if coords.dtype != torch.float32:
+        raise RuntimeError(f"CorrBlock1D: coords dtype {coords.dtype} != float32 (model.py:275)")
+    B, _, H, W1 = coords.shape
+    ld = _shear_ld(W1)
+    if B * H * _lib.shear_rows(W2, W1, 0) * ld != sheared[0].numel():
+        raise RuntimeError(f"CorrBlock1D: coords {tuple(coords.shape)} do not match the volume "
+                           "(view at model.py:312)")
+    if coords.device != sheared[0].device:
+        raise RuntimeError("CorrBlock1D: coords and pyramid on different devices")
+    x = coords[:, 0]
+    if x.stride(2) != 1 or x.stride(1) != W1:
+        x = x.contiguous()
+    cbs = x.stride(0) if B > 1 else H * W1
+    out = torch.empty((B, num_levels * (2 * radius + 1), H, W1), dtype=torch.float32, device=coords.device)
+    if B * H * W1 == 0:
+        return out
+    ptrs = [sheared.get(l) if l in (0, 2) else None for l in range(num_levels)]
+    ptrs = _lib.ptr_array([None if t is None else t.data_ptr() for t in ptrs])
+    widths = _lib.int_array([W2 >> l for l in range(num_levels)])
+    lds = _lib.long_array([ld if l in (0, 2) else W2 >> l for l in range(num_levels)])
+    with torch.cuda.device(coords.device):
+        rc = _lib.lib().rc_corr_lookup_chain(
+            ptrs, widths, lds, _lib.RC_F32 | _lib.RC_LAYOUT_DISPARITY, num_levels, radius, x.data_ptr(),
+            cbs, B, H, W1, out.data_ptr(), _stream(coords.device))
+    _lib.check(rc, "rc_corr_lookup_chain")
+    return out
+
+
 # ----------------------------------------------------------------- backward
 
 class _GradLevels(list):
@@ -641,9 +739,23 @@ class CorrBlock1D:
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
                  lazy_levels=None, shadow=None, channels_last=False, low_latency=False,
-                 grad_shadow=None, exact_f32=False, grad_deferred=None):
+                 grad_shadow=None, exact_f32=False, grad_deferred=None, layout="rows"):
         self.num_levels = num_levels
         self.radius = radius
+        # layout="disparity" (opt-in, RC_LAYOUT_DISPARITY): the
+        # stored levels 0 and 2 disparity-major, so a wave's pixels that look
+        # at the same disparity read contiguous memory; the same values and
+        # lookups bit for bit, faster on the network's coherent coordinates,
+        # slower on independent random ones.  corr_pyramid is gathered into
+        # the reference's rows when read.
+        if layout not in ("rows", "disparity"):
+            raise ValueError(f"CorrBlock1D: layout={layout!r}: 'rows' or 'disparity'")
+        self.layout = layout
+        self._sheared = None
+        if layout == "disparity":
+            self._init_sheared(fmap1, fmap2, num_levels, radius, pyramid_dtype, lazy_levels, shadow,
+                               channels_last, low_latency, grad_shadow, exact_f32, grad_deferred)
+            return
         # lookup outputs in NHWC memory order (torch.channels_last): same
         # shape and values; written by the pair kernel as contiguous per-wave
         # runs instead of one 256-B piece per channel plane
@@ -725,12 +837,44 @@ class CorrBlock1D:
                                      deferred=grad_deferred, exact_f32=exact_f32)
             self._token = _BuildFn.apply(fmap1, fmap2, self._state)
 
+    def _init_sheared(self, fmap1, fmap2, num_levels, radius, pyramid_dtype, lazy_levels, shadow,
+                      channels_last, low_latency, grad_shadow, exact_f32, grad_deferred):
+        if pyramid_dtype is None:
+            pyramid_dtype = torch.float32
+        why = shear_supported(fmap1, fmap2, num_levels, radius, pyramid_dtype)
+        if why is None and (channels_last or low_latency or shadow or grad_shadow or exact_f32
+                            or lazy_levels is False):
+            why = ("the default options only (NCHW output, no low_latency, shadow, grad_shadow, "
+                   "exact_f32 or eager levels)")
+        if why is not None:
+            raise ValueError(f"CorrBlock1D(layout='disparity'): {why}")
+        self.pyramid_dtype = pyramid_dtype
+        self.channels_last = False
+        B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+        self._shape = (B, H, W1, W2)
+        self._chain, self._shadow = True, frozenset()
+        grad = torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad)
+        with torch.no_grad():
+            self._sheared = build_sheared(fmap1, fmap2, num_levels)
+        self._levels = [None] * (num_levels + 1)
+        self._state = self._token = None
+        if grad:
+            self._state = _GradState(B * H * W1, [W2 >> i for i in range(num_levels)], fmap1.device,
+                                     num_levels, radius, None, deferred=grad_deferred)
+            self._token = _BuildFn.apply(fmap1, fmap2, self._state)
+
     @property
     def corr_pyramid(self):
         """num_levels+1 tensors (B*H*W1, 1, 1, W2 >> l) as model.py:287-295;
-        lazily pooled levels are built on first access."""
+        lazily pooled levels are built on first access (layout="disparity":
+        the stored levels gathered into rows, the others pooled from them)."""
         if any(t is None for t in self._levels):
             with torch.no_grad():
+                if self._sheared is not None:
+                    B, H, W1, W2 = self._shape
+                    for l, S in self._sheared.items():
+                        if self._levels[l] is None:
+                            self._levels[l] = unshear_level(S, l, B, H, W1, W2)
                 for l in range(1, len(self._levels)):
                     if self._levels[l] is None:
                         self._levels[l] = pool_level(self._levels[l - 1])
@@ -738,8 +882,10 @@ class CorrBlock1D:
 
     @property
     def levels_stored(self):
-        """Indices of the pyramid levels currently held in memory."""
-        return [l for l, t in enumerate(self._levels) if t is not None]
+        """Indices of the pyramid levels currently held in memory (either
+        layout)."""
+        held = set(self._sheared or ())
+        return sorted(held | {l for l, t in enumerate(self._levels) if t is not None})
 
     @corr_pyramid.setter
     def corr_pyramid(self, levels):
@@ -747,6 +893,8 @@ class CorrBlock1D:
         self._levels = list(levels)
         self._chain = False
         self._shadow = frozenset()
+        self._sheared = None
+        self.layout = "rows"
 
     def _read_levels(self):
         """Levels 0 .. num_levels-1 for the per-level kernels (the ones a
@@ -757,6 +905,8 @@ class CorrBlock1D:
         return self.corr_pyramid[:L]
 
     def _lookup(self, coords):
+        if self._sheared is not None:
+            return lookup_sheared(self._sheared, coords, self.num_levels, self.radius, self._shape[3])
         if self._chain:
             return lookup_chain(self._levels, coords, self.num_levels, self.radius, self._shadow,
                                 self.channels_last)
@@ -778,6 +928,8 @@ class CorrBlock1D:
         updates in place.  Inference only."""
         if self._token is not None and torch.is_grad_enabled():
             raise RuntimeError("CorrBlock1D.lookup_step is inference-only")
+        if self._sheared is not None:
+            raise RuntimeError("CorrBlock1D.lookup_step: not available with layout='disparity'")
         _check_coords(self._levels, coords1)
         B, C2, H, W1 = coords1.shape
         if C2 != 2:
@@ -828,6 +980,8 @@ class CorrBlock1D:
         if torch.is_grad_enabled() and (self._token is not None or weight.requires_grad):
             raise RuntimeError("CorrBlock1D.lookup_convc1 is inference-only; use "
                                "convc1(block(coords)) when gradients are needed")
+        if self._sheared is not None:
+            raise RuntimeError("CorrBlock1D.lookup_convc1: not available with layout='disparity'")
         return lookup_convc1(self._read_levels(), coords, self.num_levels, self.radius, weight,
                              bias, relu)
 

@@ -37,12 +37,16 @@ long long shadow_offset(long long rows, long long ld, int esize) { return RC_SHA
 
 // pyr_dtype bits an entry point accepts: the element type (low byte), the
 // RC_SHADOW_LEVEL bits and, where the pair kernel serves it, RC_OUT_CHANNELS_LAST.
-int check_flags(const char *who, int pyr_dtype, bool allow_cl, bool build = false) {
+int check_flags(const char *who, int pyr_dtype, bool allow_cl, bool build = false, bool allow_disp = false) {
     const unsigned known = 0xFFu | RC_SHADOW | (allow_cl ? (unsigned)RC_OUT_CHANNELS_LAST : 0u) |
-                           (build ? (unsigned)RC_BUILD_EXACT_F32 : 0u);
+                           (build ? (unsigned)RC_BUILD_EXACT_F32 : 0u) |
+                           (allow_disp ? (unsigned)RC_LAYOUT_DISPARITY : 0u);
     if (!allow_cl && (pyr_dtype & RC_OUT_CHANNELS_LAST))
         return fail(RC_EUNSUPPORTED, "%s: RC_OUT_CHANNELS_LAST is only defined for "
                     "rc_corr_lookup_chain / rc_corr_lookup_step", who);
+    if (!allow_disp && (pyr_dtype & RC_LAYOUT_DISPARITY))
+        return fail(RC_EUNSUPPORTED, "%s: RC_LAYOUT_DISPARITY is only defined for "
+                    "rc_corr_build / rc_corr_lookup_chain", who);
     if ((unsigned)pyr_dtype & ~known)
         return fail(RC_EINVAL, "%s: unknown pyr_dtype flag bits 0x%x", who, (unsigned)pyr_dtype & ~known);
     return RC_OK;
@@ -63,8 +67,9 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
                              int H, int W1, int W2, void *const *pyr, const long *pyr_ld, int nbuf,
                              int pyr_dtype, void *stream) {
     g_err[0] = 0;
-    if (int e = check_flags("rc_corr_build", pyr_dtype, false, true)) return e;
+    if (int e = check_flags("rc_corr_build", pyr_dtype, false, true, true)) return e;
     const bool exact_f32 = (pyr_dtype & RC_BUILD_EXACT_F32) != 0;
+    const bool disp = (pyr_dtype & RC_LAYOUT_DISPARITY) != 0;
     const unsigned shmask = ((unsigned)pyr_dtype >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits
     pyr_dtype &= 0xFF;
     if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
@@ -82,6 +87,24 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     if (pyr_dtype != RC_F32 && pyr_dtype != RC_BF16)
         return fail(RC_EINVAL, "rc_corr_build: unknown pyramid dtype %d", pyr_dtype);
     if (!pyr) return fail(RC_EINVAL, "rc_corr_build: null pyramid array");
+    if (disp) {   // RC_LAYOUT_DISPARITY: the split build's pair layout only
+        if (fmap_dtype != RC_F32 || pyr_dtype != RC_F32 || exact_f32 || shmask)
+            return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_DISPARITY needs fp32 fmaps and pyramid, "
+                        "the split build and no shadow copies");
+        if (!(nbuf == 1 || (nbuf == 3 && !pyr[1])))
+            return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_DISPARITY stores the pair layout: "
+                        "nbuf 1, or 3 with pyr[1] NULL");
+        if (W1 % 4 || W2 % 4)
+            return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_DISPARITY needs W1, W2 multiples of 4");
+        if (!pyr_ld) return fail(RC_EINVAL, "rc_corr_build: RC_LAYOUT_DISPARITY needs pyr_ld");
+        for (int l = 0; l < nbuf; l += 2) {
+            if (pyr_ld[l] < W1 || pyr_ld[l] % 4)
+                return fail(RC_EINVAL, "rc_corr_build: disparity-major row stride %ld of level %d must be "
+                            ">= W1 = %d and a multiple of 4", pyr_ld[l], l, W1);
+            if ((long long)B * H * RC_SHEAR_ROWS(W2, W1, l) * pyr_ld[l] * 4 >= 0xFFFFFF00LL)
+                return fail(RC_EUNSUPPORTED, "rc_corr_build: disparity-major level %d exceeds 4 GiB", l);
+        }
+    }
     if ((long long)B * H * W1 == 0) return RC_OK;
     if (!fmap1 || !fmap2 || !aligned16(fmap1) || !aligned16(fmap2))
         return fail(RC_EINVAL, "rc_corr_build: feature maps must be non-null and 16-byte aligned");
@@ -93,7 +116,7 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
         if (!pyr[l] && may_skip) continue;
         if (!pyr[l] || !aligned16(pyr[l]))
             return fail(RC_EINVAL, "rc_corr_build: pyramid buffer %d null or not 16-byte aligned", l);
-        if (pyr_ld && pyr_ld[l] < (long)(W2 >> l))
+        if (!disp && pyr_ld && pyr_ld[l] < (long)(W2 >> l))
             return fail(RC_EINVAL, "rc_corr_build: row stride %ld of level %d < width %d", pyr_ld[l],
                         l, W2 >> l);
     }
@@ -108,6 +131,7 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
         a.ld[l] = pyr_ld ? pyr_ld[l] : (W2 >> l);
         if ((shmask >> l & 1u) && pyr[l])
             a.shadow[l] = shadow_offset((long long)B * H * W1, a.ld[l], pyr_dtype == RC_BF16 ? 2 : 4);
+        if (disp && pyr[l]) a.shk[l] = RC_SHEAR_ROWS(W2, W1, l);
     }
     a.tiles_m = (W1 + 127) / 128;
     a.tiles_n = (W2 + 127) / 128;
@@ -128,6 +152,8 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     hipError_t e = hipErrorNotSupported;
     if (bf16_mma) e = rc_launch_build_bf16mma(a, fmap_dtype == RC_BF16, s);
     else if (!exact_f32) e = rc_launch_build_split(a, s);
+    if (e == hipErrorNotSupported && disp)
+        return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_DISPARITY: shape outside the split build");
     if (e == hipErrorNotSupported && !bf16_mma) e = rc_launch_build_f32(a, s);
     int rc = hip_rc(e, "rc_corr_build: volume launch");
     if (rc) return rc;
@@ -172,6 +198,7 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
                 long coord_batch_stride, int B, int H, int W1, const float *out, rc::LookupArgs &a,
                 bool *empty, bool allow_null = false) {
     *empty = false;
+    const bool disp = (pyr_dtype & RC_LAYOUT_DISPARITY) != 0;     // rows of W1 (or more) per diagonal
     const unsigned shmask = ((unsigned)pyr_dtype >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits
     pyr_dtype &= 0xFF;
     if (levels < 1 || levels > RC_MAX_LEVELS)
@@ -204,6 +231,15 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
         a.lvl[i] = pyr[i];
         a.W[i] = widths[i];
         a.ld[i] = pyr_ld ? pyr_ld[i] : widths[i];
+        if (disp) {
+            if (a.ld[i] < W1 || a.ld[i] % 4)
+                return fail(RC_EINVAL, "%s: disparity-major row stride %lld of level %d must be >= W1 = %d "
+                            "and a multiple of 4", who, a.ld[i], i, W1);
+            a.shk[i] = RC_SHEAR_ROWS(widths[0], W1, i);
+            if ((long long)B * H * a.shk[i] * a.ld[i] * 4 >= 0xFFFFFF00LL)
+                return fail(RC_EUNSUPPORTED, "%s: disparity-major level %d exceeds 4 GiB", who, i);
+            continue;
+        }
         if (a.ld[i] < widths[i])
             return fail(RC_EINVAL, "%s: level %d row stride %lld < width %d", who, i, a.ld[i],
                         widths[i]);
@@ -219,6 +255,7 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
     a.cbs = coord_batch_stride;
     a.P = P;
     a.HW = H * W1;
+    a.W1 = W1;
     a.levels = levels;
     return RC_OK;
 }
@@ -289,14 +326,19 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
-    if (int e = check_flags("rc_corr_lookup_chain", pyr_dtype, true)) return e;
+    if (int e = check_flags("rc_corr_lookup_chain", pyr_dtype, true, false, true)) return e;
     int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty, true);
     if (rc) return rc;
     const bool cl = (pyr_dtype & RC_OUT_CHANNELS_LAST) != 0;
+    const bool disp = (pyr_dtype & RC_LAYOUT_DISPARITY) != 0;
+    const bool shadowed = ((unsigned)pyr_dtype & RC_SHADOW) != 0;
     pyr_dtype &= 0xFF;
     bool pair;
     if ((rc = chain_kind("rc_corr_lookup_chain", pyr, widths, levels, radius, &pair))) return rc;
+    if (disp && (!pair || pyr_dtype != RC_F32 || cl || shadowed))
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: RC_LAYOUT_DISPARITY needs the fp32 pair layout "
+                    "(2 levels, or 4 with level 2 given), NCHW output and no shadow copies");
     if (pyr_dtype == RC_BF16 && !pair)
         return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: a bf16 pyramid needs the pair layout "
                     "(2 levels, or 4 with level 2 given)");

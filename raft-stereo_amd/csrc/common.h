@@ -120,6 +120,9 @@ struct BuildArgs {
     // line-phase shadow copies (ABI v5, RC_SHADOW): a stored level l is also
     // written at (char*)lvl[l] + shadow[l] bytes (0 = no copy)
     long long shadow[kMaxLevels];
+    // RC_LAYOUT_DISPARITY (ABI v9): levels 0 and 2 disparity-major, shk[l]
+    // rows (diagonals) of ld[l] elements per row block; 0 = row layout
+    long long shk[kMaxLevels];
 };
 
 struct LookupArgs {
@@ -144,6 +147,9 @@ struct LookupArgs {
     // (0 = none); read by the pair kernel (RC_SHADOW, ABI v5)
     long long shadow[kMaxLevels];
     int out_cl;               // channels-last output out[p*C + ch] (pair kernel; ABI v5)
+    // RC_LAYOUT_DISPARITY (ABI v9): levels 0 and 2 disparity-major, shk[l]
+    // rows (diagonals) of ld[l] elements per row block; 0 = row layout
+    long long shk[kMaxLevels];
 };
 
 // Backward of the lookup: level gradients (fp32, row stride ld[i] % 4 == 0).

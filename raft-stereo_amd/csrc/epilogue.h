@@ -12,7 +12,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Dev-only ablation flags (RAFTCORR_BUILD_MODE): 1 = no operand loads,
 // 2 = no epilogue stores.  Product launches use 0.
 enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8, kModeNoFragReads = 16,
-       kModeStagger = 64, kModeNoMfma = 512, kModeNoSplit = 1024, kModeSpread = 2048, kModePackedSub = 8192,
+       kModeStagger = 64, kModeNoMfma = 512, kModeNoSplit = 1024, kModeSpread = 2048, kModeSheared = 4096,
+       kModePackedSub = 8192,
        kModeL2Stores = 65536, kModeDirect = 131072, kModeFastEpi = 262144, kModeGenericEpi = 524288,
        kModePairEpi = 1048576 };
 
@@ -225,6 +226,124 @@ __device__ __forceinline__ void flush_store(const FlushRegs<CW, L> &f, const Bui
         if (lok && R < 16 && w1 < w1e) {
             const float v[4] = {f.x[k][0], f.x[k][1], f.x[k][2], f.x[k][3]};
             store_vec<4>(a.lvl[L], false, (rowbase + w1) * a.ld[L] + col, v, a.shadow[L]);
+        }
+    }
+}
+
+// Disparity-major stores (RC_LAYOUT_DISPARITY, ABI v9) of the pair layout's
+// levels 0 and 2: level i of row block `row` is S_i[k][w1] with
+// k = (w1 >> i) - j + (W2 >> i) - 1, row stride a.ld[i], a.shk[i] rows per
+// block, so the pixels of one image row that look at the same disparity read
+// one contiguous run of a row of S_i.  The values and their pooling order are
+// epilogue_swapped's (the same bits, elsewhere); level 1 is pooled but not
+// stored.  Per fragment column nb the wave stages its 16 x WT level-0 values
+// (pitch WT + 4) and 16 x WT/4 level-2 values (pitch WT/4 + 4) in LDS and
+// writes them along diagonals, one lane per 4 consecutive w1 of a diagonal:
+// a 16-B store when all four lie in the wave's block (w1 < w1e, j inside
+// [n0, n0 + WT) and < W2 >> i), else one dword per element that does.  A
+// diagonal's 64-B piece of an nb joins the piece of the next nb in L2.
+template <int STRIDE>     // four floats STRIDE floats apart, one wait
+__device__ __forceinline__ void sheared_rd4(uint32_t a0, float (&x)[4]) {
+    asm volatile("ds_read_b32 %0, %4\n\tds_read_b32 %1, %4 offset:%5\n\t"
+                 "ds_read_b32 %2, %4 offset:%6\n\tds_read_b32 %3, %4 offset:%7\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+                 : "v"(a0), "i"(4 * STRIDE), "i"(8 * STRIDE), "i"(12 * STRIDE));
+}
+
+template <int FMA>
+__device__ __forceinline__ void epilogue_sheared(f32x4 (&acc)[FMA][4], const BuildArgs &a, int row, int m0,
+                                                 int n0, int lane, uint32_t st0, int w1e) {
+    constexpr int WT = 16 * FMA, P0 = WT + 4, P2 = WT / 4 + 4;
+    constexpr int ND = WT + 15;                     // level-0 diagonals of a 16 x WT block
+    constexpr int NS0 = 4 * ND;                     // (w1 group, diagonal) slots
+    constexpr uint32_t S2OFF = 16 * P0 * 4;         // level-2 image after the level-0 one
+    const int g = lane >> 4, i = lane & 15;
+    const int W0 = a.W2, Wq = a.W2 >> 2;
+    const bool lv2 = a.nfused >= 3 && a.lvl[2] != nullptr;
+    float *S0 = static_cast<float *>(a.lvl[0]) + (long long)row * a.shk[0] * a.ld[0];
+    float *S2 = lv2 ? static_cast<float *>(a.lvl[2]) + (long long)row * a.shk[2] * a.ld[2] : nullptr;
+    // one loop body for the four columns (code size): column nb is always
+    // acc[.][0], the others move down one per pass (no dynamic register index)
+#pragma unroll 1
+    for (int nb = 0; nb < 4; ++nb) {
+        const int w1_0 = m0 + 16 * nb;
+        float v[FMA][4];
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[ma][r] = acc[ma][0][r];
+            apply_scale(v[ma], a);
+            acc[ma][0] = acc[ma][1];
+            acc[ma][1] = acc[ma][2];
+            acc[ma][2] = acc[ma][3];
+        }
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma)
+            lds_st4(st0 + 4 * (i * P0 + 16 * ma + 4 * g), f32x4{v[ma][0], v[ma][1], v[ma][2], v[ma][3]});
+        if (lv2) {
+#pragma unroll
+            for (int ma = 0; ma < FMA; ++ma) {
+                const float s2 = pool2(pool2(v[ma][0], v[ma][1], false), pool2(v[ma][2], v[ma][3], false), false);
+                lds_st1(st0 + S2OFF + 4 * (i * P2 + 4 * ma + g), s2);
+            }
+        }
+        // level 0: slot s = q + 4 dd, rows w1l = 4q + r, diagonal d = w1l - jl
+#pragma unroll
+        for (int s0 = 0; s0 < NS0; s0 += 64) {
+            const int s = s0 + lane;
+            const int q = s & 3, d = (s >> 2) - (WT - 1);
+            bool ok[4], all = s < NS0;
+            int jl0 = 4 * q - d;                            // jl of r = 0
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jl = jl0 + r;
+                ok[r] = s < NS0 && jl >= 0 && jl < WT && n0 + jl < W0 && w1_0 + 4 * q + r < w1e;
+                all = all && ok[r];
+            }
+            const int jc = jl0 < 0 ? 0 : (jl0 > WT - 4 ? WT - 4 : jl0);   // an address inside the image
+            float x[4];
+            sheared_rd4<P0 + 1>(st0 + 4 * ((4 * q) * P0 + jc), x);
+            const long long k = (long long)(w1_0 - n0 + d + W0 - 1);
+            float *dst = S0 + k * a.ld[0] + (w1_0 + 4 * q);
+            if (all) {
+                *reinterpret_cast<f32x4 *>(dst) = f32x4{x[0], x[1], x[2], x[3]};
+            } else if (s < NS0 && (ok[0] || ok[1] || ok[2] || ok[3])) {
+                // the clamped address read other elements: re-read the exact ones
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (!ok[r]) continue;
+                    float y;
+                    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                                 : "=v"(y) : "v"(st0 + 4 * ((4 * q + r) * P0 + jl0 + r)));
+                    dst[r] = y;
+                }
+            }
+        }
+        if (lv2) {
+            // level 2: slot = q + 4 j2l; rows 4q..4q+3 share the column
+#pragma unroll
+            for (int s0 = 0; s0 < WT; s0 += 64) {
+                const int s = s0 + lane;
+                const int q = s & 3, j2l = s >> 2;
+                bool ok[4], all = s < WT && (n0 >> 2) + j2l < Wq;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    ok[r] = all && w1_0 + 4 * q + r < w1e;
+                }
+                const bool any = ok[0];
+                all = ok[0] && ok[1] && ok[2] && ok[3];
+                float x[4];
+                sheared_rd4<P2>(st0 + S2OFF + 4 * ((4 * q) * P2 + (j2l < WT / 4 ? j2l : 0)), x);
+                const long long k = (long long)(((w1_0 >> 2) + q) - ((n0 >> 2) + j2l) + Wq - 1);
+                float *dst = S2 + k * a.ld[2] + (w1_0 + 4 * q);
+                if (all) {
+                    *reinterpret_cast<f32x4 *>(dst) = f32x4{x[0], x[1], x[2], x[3]};
+                } else if (any) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (ok[r]) dst[r] = x[r];
+                }
+            }
         }
     }
 }

@@ -765,6 +765,121 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// finish_pair's memory path over the disparity-major layout: every tap of
+// level lo (stored) and lo + 1 (its pairwise means) re-read, the fp32 ops of
+// level_taps_mem.
+template <int R, class Sink>
+__device__ __forceinline__ void sheared_taps_mem(const LookupArgs &a, int lo, float x, long long bh, int w1,
+                                                 Sink &&sink) {
+    constexpr int T = 2 * R + 1;
+    const float *S = static_cast<const float *>(a.lvl[lo]) + bh * a.shk[lo] * a.ld[lo];
+    const int W0 = a.W[lo];
+    const long long base = (long long)((w1 >> lo) + W0 - 1);        // row of element 0 is base - j
+    auto elem = [&](long long j) { return S[(base - j) * a.ld[lo] + w1]; };
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const int W = a.W[lo + half];
+        const float Wm1 = (float)(W - 1), hw = Wm1 / 2.0f;
+        const DivRN dv = div_prep(Wm1);
+        const float xl = x / (float)(1 << (lo + half));
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + xl;
+            const float xn = div_rn(2.0f * xt, dv) - 1.0f;
+            const float xp = (xn + 1.0f) * hw;
+            const float x0 = floorf(xp);
+            const float wt1 = xp - x0, wt0 = 1.0f - wt1;
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            const long long e = (long long)x0;
+            float v0 = 0.0f, v1 = 0.0f;
+            if (half == 0) {
+                if (ok0) v0 = elem(e);
+                if (ok1) v1 = elem(e + 1);
+            } else {
+                if (ok0) v0 = (elem(2 * e) + elem(2 * e + 1)) * 0.5f;
+                if (ok1) v1 = (elem(2 * e + 2) + elem(2 * e + 3)) * 0.5f;
+            }
+            sink((lo + half) * T + t, fmaf(wt1, v1, wt0 * v0));
+        }
+    }
+}
+
+// ---- lookup over a disparity-major pair layout (RC_LAYOUT_DISPARITY) ----
+// The pair kernel's arithmetic (levels 0 and 2 stored, 1 and 3 their
+// pairwise means, finish_pair: bit-identical) over levels stored as
+// S_i[b,h][k][w1], k = (w1 >> i) - j + W_i - 1 (rc_corr_build with the
+// flag; a.shk[i] rows of a.ld[i] floats per image row): the lanes of a wave
+// whose pixels look at the same disparity read one contiguous run of a row
+// per span element -- coalesced along w1 -- instead of a 16-B piece of 64
+// different pixel rows.  A span is 2(2r+4) dword loads per lane (exact-span
+// predicated).  Faster than the row layout where neighbouring pixels' coords
+// agree (the network's own fields), slower on independent random ones
+// (DESIGN.md §3.2h).
+template <int R, int NL>
+__global__ __launch_bounds__(256) void lookup_sheared_pair_kernel(LookupArgs a) {
+    static_assert(NL == 2 || NL == 4, "pair lookup: 2 or 4 levels");
+    constexpr int NP = NL / 2, NS = PairSpan<R>::NS;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const long long pblk = (long long)blk * 256;
+    const long long p = pblk + threadIdx.x;
+    const bool active = p < a.P;
+    const long long pp = active ? p : a.P - 1;
+    const long long bimg = pp / a.HW, rem = pp - bimg * a.HW;
+    const float x = pixel_x(a, bimg, rem, active);
+    const int H = a.HW / a.W1;
+    const int h = (int)(rem / a.W1), w1 = (int)(rem - (long long)h * a.W1);
+    const long long bh = bimg * H + h, bh0 = pblk / a.W1;          // bh0: block-uniform
+    float *outp = a.out + bimg * (long long)(NL * (2 * R + 1)) * a.HW + rem;
+    auto sink = [&](int ch, float v) {
+        if (active) outp[(long long)ch * a.HW] = v;
+    };
+    PairSpan<R> sp[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const int lo = 2 * k;
+        PairSpan<R> &ps = sp[k];
+        const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+        const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+        ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));
+        ps.m = ps.inwin ? floorf(xhi) : 0.0f;
+        ps.n = ps.inwin ? floorf(xlo) : 0.0f;
+        const int dd = (int)ps.n - 2 * (int)ps.m;
+        ps.valid = ps.inwin && (dd == 0 || dd == 1);
+        int lo_e = 0x7FFFFFFF, hi_e = -1;
+        if (ps.inwin) {
+            int f, l;
+            tap_span<R>(xlo, Wlo, f, l);
+            if (f <= l) { lo_e = f; hi_e = l; }
+            tap_span<R>(xhi, Whi, f, l);
+            if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
+        }
+        ps.sh = 0;
+        const int sa = 2 * ((int)ps.m - R - 1);
+        const long long K = a.shk[lo], ldw = a.ld[lo];
+        const float *lv = static_cast<const float *>(a.lvl[lo]);
+        const auto rs = make_rsrc(lv + bh0 * K * ldw, clamp_bytes((a.P / a.W1 - bh0) * K * ldw * 4));
+        const long long rowk = (bh - bh0) * K + (w1 >> lo) + Wlo - 1;    // row of element 0
+#pragma unroll
+        for (int c = 0; c < PairSpan<R>::NC * 4; ++c) {
+            const int j = sa + c;
+            const bool ok = c < NS && j >= lo_e && j <= hi_e;
+            const uint32_t off = ok ? (uint32_t)(((rowk - j) * ldw + w1) * 4) : 0xFFFFFF00u;
+            ps.q[c >> 2][c & 3] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+        }
+    }
+    // a subnormal x (the only way to break n = 2m + dd) takes the memory path
+    // of finish_pair, which reads the row layout: not available here, so the
+    // taps of such a lane come from sheared_taps_mem below instead
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        if (__builtin_expect(sp[k].inwin && !sp[k].valid, 0)) {
+            sheared_taps_mem<R>(a, 2 * k, x, bh, w1, sink);
+            continue;
+        }
+        finish_pair<R, true>(sp[k], a, 2 * k, x, pp, sink);
+    }
+}
+
 template <int R, int NL, bool BF16, bool EXACT, int BS = 256, int WPE = 1>
 static void launch_k(const LookupArgs &a, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + BS - 1) / BS);
@@ -847,6 +962,13 @@ static hipError_t launch_chain_m(const LookupArgs &a, hipStream_t s, unsigned ld
 template <int R>
 static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    if (a.shk[0]) {   // RC_LAYOUT_DISPARITY (fp32, NCHW output: checked by the C-ABI)
+        if (bf16 || a.out_cl) return hipErrorNotSupported;
+        if (a.levels == 4) hipLaunchKernelGGL((lookup_sheared_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);
+        else if (a.levels == 2) hipLaunchKernelGGL((lookup_sheared_pair_kernel<R, 2>), dim3(nblk), dim3(256), 0, s, a);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
 #ifdef RAFTCORR_DEV
     if (const hipError_t e = dev_launch_pair<R>(a, bf16, s); e != hipErrorNotSupported) return e;
 #endif

@@ -139,13 +139,19 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if constexpr (FA > 0)
+    if constexpr (FA > 0 && (MODE & kModeSheared) != 0) {
+        // RC_LAYOUT_DISPARITY: levels 0 and 2 written disparity-major
+        const int w1e = c.M0 + c.o1 + 16 * FB;
+        epilogue_sheared<FA>(acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
+                             lds_u32(smem + c.wave * (kSpSL * kSpSlot / 4)), w1e < a.W1 ? w1e : a.W1);
+    } else if constexpr (FA > 0) {
         // the compile-time-geometry flushes (fp32 levels 0-2) unless the dev
         // A/B asks for the generic epilogue: config 2 262.5 vs 281.2 us
         // (profiles/r04/o/build_ablate.log, bit-identical)
         epilogue_swapped<FA, (MODE & kModeGenericEpi) ? MODE : (MODE | kModeFastEpi), NLM>(
             acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
             lds_u32(smem + c.wave * (kSpSL * kSpSlot / 4)), c.M0 + c.o1 + 16 * FB);
+    }
 }
 
 template <int FA, int MODE, int NLM>
@@ -245,6 +251,11 @@ hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s) {
     if (const hipError_t e = rc::dev_launch_build_split(a, nwg, tf1, tf2, tiles1, tiles2, s); e != hipErrorNotSupported)
         return e;
 #endif
+    if (a.shk[0]) {   // disparity-major levels 0 and 2 (the caller checked the pair layout)
+        hipLaunchKernelGGL((rc::build_split_kernel<rc::kModeSheared, 3>), dim3((unsigned)nwg), dim3(256), 0, s, a,
+                           (int)nwg, tf1, tf2, tiles1, tiles2);
+        return hipGetLastError();
+    }
     // up to 3 fused levels (the pair layout: 0 and 2 stored) keeps the
     // epilogue's level pointers out of the scalar registers
     if (a.nfused <= 3)

@@ -220,3 +220,51 @@ def test_backward_entry_points_reject_unknown_flag_bits():
     assert L.rc_corr_lookup_backward_calls(pair, w, None, 4 | _lib.RC_GRAD_OVERWRITE, 4, 0, None, None,
                                            1, 2, 64, None, None) == _lib.RC_EINVAL
     assert b"no calls" in L.rc_last_error()
+
+
+def test_disparity_layout_flag_validation():
+    """RC_LAYOUT_DISPARITY (ABI v9): the header's value and RC_SHEAR_ROWS
+    agree with the binding; only rc_corr_build and rc_corr_lookup_chain take
+    it, and only for the fp32 pair layout on the split build -- every other
+    request is refused before any launch (B = 0: nothing is touched)."""
+    text = open(_lib.HEADER).read()
+    m = re.search(r"#define RC_LAYOUT_DISPARITY\s+(0x[0-9a-fA-F]+)", text)
+    assert m and int(m.group(1), 16) == _lib.RC_LAYOUT_DISPARITY
+    assert "#define RC_SHEAR_ROWS(W2, W1, l) (((W2) >> (l)) + (((W1) - 1) >> (l)))" in text
+    assert _lib.shear_rows(240, 240, 0) == 479 and _lib.shear_rows(240, 240, 2) == 119
+    L = _lib.lib()
+    f = lambda a: ctypes.c_void_p(a)  # noqa: E731
+    D = _lib.RC_F32 | _lib.RC_LAYOUT_DISPARITY
+    one = _lib.ptr_array([f(0x1000)])
+    w1 = _lib.int_array([64])
+    assert L.rc_corr_lookup(one, w1, None, D, 1, 4, f(0x2000), 0, 0, 1, 64, f(0x3000), None) == \
+        _lib.RC_EUNSUPPORTED
+    assert b"RC_LAYOUT_DISPARITY" in L.rc_last_error()
+    assert L.rc_corr_lookup_conv(one, w1, None, D, 1, 4, f(0x2000), 0, 0, 1, 64, f(0x4000), None, 4, 1,
+                                 f(0x3000), None) == _lib.RC_EUNSUPPORTED
+    assert L.rc_corr_pool(None, 8, None, 4, 0, 8, D, None) == _lib.RC_EUNSUPPORTED
+    pair = _lib.ptr_array([f(0x1000), None, f(0x2000), None])
+    w4 = _lib.int_array([64, 32, 16, 8])
+    assert L.rc_corr_lookup_step(pair, w4, None, D, 4, 4, 1, f(0x2000), None, f(0x3000), f(0x5000),
+                                 0, 1, 64, f(0x4000), None) == _lib.RC_EUNSUPPORTED
+    chain = lambda ptrs, w, dt, lv, r=4: L.rc_corr_lookup_chain(  # noqa: E731
+        ptrs, w, None, dt, lv, r, f(0x2000), 0, 0, 1, 64, f(0x3000), None)
+    assert chain(pair, w4, D, 4) == _lib.RC_OK                              # B = 0, accepted
+    three = _lib.ptr_array([f(0x1000), f(0x2000), None])
+    assert chain(three, _lib.int_array([64, 32, 16]), D, 3) == _lib.RC_EUNSUPPORTED
+    assert chain(pair, w4, _lib.RC_BF16 | _lib.RC_LAYOUT_DISPARITY, 4) == _lib.RC_EUNSUPPORTED
+    assert chain(pair, w4, D | _lib.RC_OUT_CHANNELS_LAST, 4) == _lib.RC_EUNSUPPORTED
+    assert chain(pair, w4, D | _lib.shadow_level(2), 4) == _lib.RC_EUNSUPPORTED
+    ld = _lib.long_array([64, 32, 64])
+    b3 = _lib.ptr_array([f(0x1000), None, f(0x2000)])
+    build = lambda **kw: L.rc_corr_build(  # noqa: E731
+        f(0x1000), f(0x2000), kw.get("dt", 0), 0, 8, 1, kw.get("W1", 64), 64, kw.get("pyr", b3),
+        kw.get("ld", ld), kw.get("nbuf", 3), kw.get("pdt", D), None)
+    assert build() == _lib.RC_OK                                            # B = 0, accepted
+    assert build(dt=_lib.RC_BF16) == _lib.RC_EUNSUPPORTED
+    assert build(pdt=D | _lib.RC_BUILD_EXACT_F32) == _lib.RC_EUNSUPPORTED
+    assert build(nbuf=2, pyr=_lib.ptr_array([f(0x1000), f(0x2000)])) == _lib.RC_EUNSUPPORTED
+    assert build(pyr=_lib.ptr_array([f(0x1000), f(0x3000), f(0x2000)])) == _lib.RC_EUNSUPPORTED
+    assert build(W1=62) == _lib.RC_EUNSUPPORTED
+    assert build(ld=None) == _lib.RC_EINVAL
+    assert build(ld=_lib.long_array([60, 32, 64])) == _lib.RC_EINVAL      # < W1

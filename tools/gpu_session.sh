@@ -149,6 +149,8 @@ has sablr && step build_ablate_realtime 300 python tools/build_ablate.py --confi
 has sablm && step build_ablate_middlebury 300 python tools/build_ablate.py --config middlebury --modes ${SABL_MODES:-0,4096} --rounds 5
 has sabl && step build_ablate 600 python tools/build_ablate.py --modes ${SABL_MODES:-0,8192} --rounds ${SABL_ROUNDS:-9} ${SABL_CONFIG:+--config $SABL_CONFIG}
 has shear && step shear_probe 600 python tools/shear_probe.py
+has tdisp && step pytest_disp 600 python -u -m pytest tests/test_disparity_gpu.py tests/test_split_gpu.py tests/test_corr_gpu.py -v -rf --timeout 120 --timeout-method thread
+has pdisp && step shear_probe_product 900 python tools/shear_probe.py --product ${SHEAR_ARGS:-}
 has gfloor && step graph_floor 300 python tools/graph_floor.py
 has train && step train_probe 300 python tools/train_probe.py
 has trainmb && step train_probe_middlebury 300 python tools/train_probe.py --config middlebury --reps 3

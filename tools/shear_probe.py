@@ -79,11 +79,81 @@ def shear_pair(pyr, B, H, W1):
     return out, K
 
 
+def product_main(a):
+    """--product: CorrBlock1D(layout="rows") against layout="disparity"
+    (the product path, RC_LAYOUT_DISPARITY) with the product library only:
+    the build alone (event-timed after a device-side sleep, as bench.py
+    times it), the 32 lookups of each field, and whole steps (build + 32
+    lookups), interleaved, medians; every lookup checked bit for bit."""
+    B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
+    res = {}
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(0)
+        f1 = torch.randn(B, D, H, W1, generator=g).cuda()
+        f2 = torch.randn(B, D, H, W2, generator=g).cuda()
+        layouts = ("rows", "disparity")
+        mk = {lay: (lambda lay=lay: CorrBlock1D(f1, f2, num_levels=L, radius=r, layout=lay)) for lay in layouts}
+        blocks = {lay: mk[lay]() for lay in layouts}
+        bt = {lay: [] for lay in layouts}
+        for _ in range(a.reps):
+            for lay in layouts:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda._sleep(3_000_000)
+                e0.record()
+                mk[lay]()
+                e1.record()
+                torch.cuda.synchronize()
+                bt[lay].append(e0.elapsed_time(e1) * 1e3)
+        res["build_us"] = {lay: statistics.median(bt[lay]) for lay in layouts}
+        print("build", {k: round(v, 1) for k, v in res["build_us"].items()}, flush=True)
+        for kind in ("random", "smooth", "slant", "zero", "net"):
+            if kind == "net":
+                from lookup_probe import net_coords
+                cs = net_coords(B, H, W1, iters, torch.device("cuda", 0))
+            else:
+                cs = make_coords(kind, B, H, W1, iters, seed=3)
+            for c in cs[:4]:
+                assert torch.equal(blocks["rows"](c), blocks["disparity"](c)), kind
+            per = {lay: [] for lay in layouts}
+            step = {lay: [] for lay in layouts}
+            for _ in range(a.reps):
+                for lay in layouts:
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(cs) + 1)]
+                    torch.cuda._sleep(3_000_000)
+                    ev[0].record()
+                    for k, c in enumerate(cs):
+                        blocks[lay](c)
+                        ev[k + 1].record()
+                    torch.cuda.synchronize()
+                    per[lay] += [ev[k].elapsed_time(ev[k + 1]) * 1e3 for k in range(len(cs))]
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda._sleep(3_000_000)
+                    e0.record()
+                    blk = mk[lay]()
+                    for c in cs:
+                        blk(c)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    step[lay].append(e0.elapsed_time(e1))
+            res[kind] = {lay: {"lookup_us": statistics.median(per[lay]),
+                               "step_ms": statistics.median(step[lay])} for lay in layouts}
+            print(kind, {lay: {k: round(v, 3) for k, v in res[kind][lay].items()} for lay in layouts},
+                  flush=True)
+        alg = bench.lookup_bytes(B * H * W1, L, r)
+        print(json.dumps({"config": a.config, "mode": "product", "alg_bytes": alg, "bit_identical": True,
+                          "disparity_MB": sum(t.numel() * 4 for t in blocks["disparity"]._sheared.values()) / 1e6,
+                          "results": res}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="sceneflow")
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--product", action="store_true",
+                    help="CorrBlock1D layout='rows' vs 'disparity' (product library), builds and steps")
     a = ap.parse_args()
+    if a.product:
+        return product_main(a)
     B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
     lib = _lib.dev_library().__enter__()   # the sheared kernel lives in the dev build only
     fn = lib.rc_dev_lookup_sheared_pair
