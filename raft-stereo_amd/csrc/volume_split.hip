@@ -59,11 +59,13 @@ struct SpCtx {
 };
 
 // DMA share of this wave per stage: rows 4w..4w+3 of both tiles, 2 rows
-// (1 KB = 64 lanes x 16 B) per instruction -> 4 instructions per stage.
-template <int MODE>
+// (TW / 2 lanes x 16 B: all 64 at TW = 128) per instruction -> 4 instructions
+// per stage.
+template <int MODE, int TW, int SL>
 __device__ __forceinline__ void sp_issue(const SpCtx &c, char *smem, int st) {
     typedef __attribute__((address_space(3))) void lds_void;
-    char *sA = smem + (st % kSpSL) * kSpSlot, *sB = sA + kSpOp;
+    using G = SpRing<TW, SL>;
+    char *sA = smem + (st % SL) * G::Slot, *sB = sA + G::Op;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r0 = 4 * c.wave + 2 * i;
@@ -72,9 +74,13 @@ __device__ __forceinline__ void sp_issue(const SpCtx &c, char *smem, int st) {
         // (out-of-range offset)
         uint32_t offA = d < c.D && c.wA ? c.oA[i] + (uint32_t)st * c.sA : 0xFFFFFF00u;
         uint32_t offB = d < c.D && c.wB ? c.oB[i] + (uint32_t)st * c.sB : 0xFFFFFF00u;
+        // lanes past the block's 2 TW floats write nothing (EXEC), so the
+        // next block is not overwritten
         if constexpr (!(MODE & kModeNoLoads)) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r1, (lds_void *)(sA + (r0 >> 1) * kSpBlk), 16, (int)offA, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r2, (lds_void *)(sB + (r0 >> 1) * kSpBlk), 16, (int)offB, 0, 0, 0);
+            if (TW == 128 || c.lane < TW / 2) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r1, (lds_void *)(sA + (r0 >> 1) * G::Blk), 16, (int)offA, 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(c.r2, (lds_void *)(sB + (r0 >> 1) * G::Blk), 16, (int)offB, 0, 0, 0);
+            }
         }
     }
 }
@@ -82,38 +88,42 @@ __device__ __forceinline__ void sp_issue(const SpCtx &c, char *smem, int st) {
 // K loop + epilogue of one wave with FA valid A fragments (w2) and FB valid B
 // fragments (w1); FA = 0: no valid columns -- the wave still issues its DMA
 // share and joins every barrier.
-template <int FA, int FB, int MODE, int NLM>
+template <int FA, int FB, int MODE, int NLM, int TW, int SL>
 __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, char *smem, int row) {
+    using G = SpRing<TW, SL>;
     const int lane = c.lane, i = lane & 15, g = lane >> 4;
     // lane (i, g) reads d rows 8(g & 1) .. +7 of stage (g >> 1) of the K step
-    const int lrow = (g & 1) * 4 * kSpBlk;               // rows 8(g&1): 4 blocks in
+    const int lrow = (g & 1) * 4 * G::Blk;               // rows 8(g&1): 4 blocks in
     f32x4 acc[FA > 0 ? FA : 1][4];
 #pragma unroll
     for (int x0 = 0; x0 < (FA > 0 ? FA : 1); ++x0)
 #pragma unroll
         for (int y0 = 0; y0 < 4; ++y0) acc[x0][y0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int KA = G::KA;
     const int nks = (c.nst + 1) >> 1;                     // K steps (the launcher pads nst to even)
-    // stages of K steps 0 and 1 in flight
+    // stages of K steps 0 .. KA - 1 in flight
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
-        if (st < c.nst) sp_issue<MODE>(c, smem, st);
+    for (int st = 0; st < 2 * KA; ++st)
+        if (st < c.nst) sp_issue<MODE, TW, SL>(c, smem, st);
     for (int ks = 0; ks < nks; ++ks) {
-        // RAW: my 8 DMA instructions of K step ks landed (K step 1, issued
-        // with K step 0 before the loop, may still fly at ks = 0; later K
-        // steps are issued after this wait); WAR: my LDS reads of K step
-        // ks - 1 are done.  Barrier.
-        if (ks == 0 && nks > 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        // RAW: my 8 DMA instructions of K step ks landed (the K steps issued
+        // after it may still fly: KA - 1 of them at ks = 0, from the
+        // prologue, KA - 2 later, since K step ks + KA - 1 is issued after
+        // this wait); WAR: my LDS reads of K step ks - 1 are done.  Barrier.
+        const int later = min(ks == 0 ? KA - 1 : KA - 2, nks - 1 - ks);
+        if (KA >= 3 && later >= 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+        else if (later >= 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (ks >= 1 && 2 * ks + 2 < c.nst) {             // K step ks + 1 into the slots of K step ks - 1
-            sp_issue<MODE>(c, smem, 2 * ks + 2);
-            sp_issue<MODE>(c, smem, 2 * ks + 3);
+        if (ks >= 1 && 2 * (ks + KA - 1) < c.nst) {      // K step ks + KA - 1 into the slots of K step ks - 1
+            sp_issue<MODE, TW, SL>(c, smem, 2 * (ks + KA - 1));
+            sp_issue<MODE, TW, SL>(c, smem, 2 * (ks + KA - 1) + 1);
         }
         if constexpr (FA > 0 && !(MODE & kModeNoMath)) {
-            const char *st = smem + ((2 * ks + (g >> 1)) % kSpSL) * kSpSlot + lrow;
+            const char *st = smem + ((2 * ks + (g >> 1)) % SL) * G::Slot + lrow;
             const char *pb = st + 4 * (c.o1 + i);                        // F1 (B): this wave's w1
-            const char *pa = st + kSpOp + 4 * (c.o2 + i);                // F2 (A): this wave's w2
+            const char *pa = st + G::Op + 4 * (c.o2 + i);                // F2 (A): this wave's w2
             auto mma6 = [&](f32x4 &c, const SplitFrag &x, const SplitFrag &y) {
                 if constexpr (MODE & kModeNoMfma) {   // dev timing probe: keep the split live
                     const u32x4s a = __builtin_bit_cast(u32x4s, x.h) ^ __builtin_bit_cast(u32x4s, x.m) ^
@@ -126,10 +136,10 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
             };
             SplitFrag fb[FB];
 #pragma unroll
-            for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE>(pb + 64 * n);
+            for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE, TW>(pb + 64 * n);
 #pragma unroll
             for (int m = 0; m < FA; ++m) {
-                const SplitFrag fa = sp_read<MODE>(pa + 64 * m);
+                const SplitFrag fa = sp_read<MODE, TW>(pa + 64 * m);
 #pragma unroll
                 for (int n = 0; n < FB; ++n) mma6(acc[m][n], fa, fb[n]);
             }
@@ -143,29 +153,35 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
         // RC_LAYOUT_DISPARITY: levels 0 and 2 written disparity-major
         const int w1e = c.M0 + c.o1 + 16 * FB;
         epilogue_sheared<FA>(acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
-                             lds_u32(smem + c.wave * (kSpSL * kSpSlot / 4)), w1e < a.W1 ? w1e : a.W1);
+                             lds_u32(smem + c.wave * G::Wave), w1e < a.W1 ? w1e : a.W1);
     } else if constexpr (FA > 0) {
         // the compile-time-geometry flushes (fp32 levels 0-2) unless the dev
         // A/B asks for the generic epilogue: config 2 262.5 vs 281.2 us
         // (profiles/r04/o/build_ablate.log, bit-identical)
         epilogue_swapped<FA, (MODE & kModeGenericEpi) ? MODE : (MODE | kModeFastEpi), NLM>(
             acc, a, row, c.M0 + c.o1, c.N0 + c.o2, lane,
-            lds_u32(smem + c.wave * (kSpSL * kSpSlot / 4)), c.M0 + c.o1 + 16 * FB);
+            lds_u32(smem + c.wave * G::Wave), c.M0 + c.o1 + 16 * FB);
     }
 }
 
-template <int FA, int MODE, int NLM>
+template <int FA, int MODE, int NLM, int TW, int SL>
 __device__ __forceinline__ void split_fb(int fb, const SpCtx &c, const BuildArgs &a, char *smem, int row) {
-    if (fb >= 4) split_body<FA, 4, MODE, NLM>(c, a, smem, row);
-    else if (fb == 3) split_body<FA, 3, MODE, NLM>(c, a, smem, row);
-    else if (fb == 2) split_body<FA, 2, MODE, NLM>(c, a, smem, row);
-    else split_body<FA, 1, MODE, NLM>(c, a, smem, row);
+    if constexpr ((TW / 16 + 1) / 2 >= 4) {            // a wave's share: ceil(TW / 32) fragments
+        if (fb >= 4) {
+            split_body<FA, 4, MODE, NLM, TW, SL>(c, a, smem, row);
+            return;
+        }
+    }
+    if (fb == 3) split_body<FA, 3, MODE, NLM, TW, SL>(c, a, smem, row);
+    else if (fb == 2) split_body<FA, 2, MODE, NLM, TW, SL>(c, a, smem, row);
+    else split_body<FA, 1, MODE, NLM, TW, SL>(c, a, smem, row);
 }
 
-template <int MODE, int NLM>
+// TW, SL: the ring geometry (SpRing); tiles at most TW wide (the launcher)
+template <int MODE, int NLM, int TW = 128, int SL = 4>
 __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nwg_total, int tf1, int tf2,
                                                              int tiles1, int tiles2) {
-    __shared__ __attribute__((aligned(16))) char smem[kSpSL * kSpSlot];
+    __shared__ __attribute__((aligned(16))) char smem[SpRing<TW, SL>::Bytes];
     SpCtx c;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c.lane = threadIdx.x & 63;
@@ -185,8 +201,9 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nw
     c.o1 = 16 * h1 * wm; c.o2 = 16 * h2 * wn;
     c.nst = 2 * ((a.D + 2 * kSpBK - 1) / (2 * kSpBK));   // whole K steps (d >= D reads zeros)
     {
-        const int w = 4 * (c.lane & 31);
-        c.dr0 = 4 * c.wave + (c.lane >> 5);
+        // lane -> (row of its 2-row block, 4 columns); lanes >= TW / 2 idle
+        const int w = 4 * (c.lane % (TW / 4));
+        c.dr0 = 4 * c.wave + (c.lane >= TW / 4 ? 1 : 0);
         c.wA = w < c.tw1;
         c.wB = w < c.tw2;
 #pragma unroll
@@ -207,11 +224,13 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildArgs a, int nw
     const int cw1 = a.W1 - (c.M0 + c.o1), cw2 = a.W2 - (c.N0 + c.o2);
     const int v1 = cw1 <= 0 ? 0 : min(n1, (cw1 + 15) >> 4), v2 = cw2 <= 0 ? 0 : min(n2, (cw2 + 15) >> 4);
     const int fa = v1 == 0 ? 0 : v2, fb = v1;
-    if (fa == 4) split_fb<4, MODE, NLM>(fb, c, a, smem, row);
-    else if (fa == 3) split_fb<3, MODE, NLM>(fb, c, a, smem, row);
-    else if (fa == 2) split_fb<2, MODE, NLM>(fb, c, a, smem, row);
-    else if (fa == 1) split_fb<1, MODE, NLM>(fb, c, a, smem, row);
-    else split_body<0, 1, MODE, NLM>(c, a, smem, row);
+    constexpr int FMAX = (TW / 16 + 1) / 2;                // fragments per wave at most (4 or 3)
+    static_assert(FMAX == 3 || FMAX == 4, "split tile width");
+    if (FMAX == 4 && fa >= 4) split_fb<FMAX, MODE, NLM, TW, SL>(fb, c, a, smem, row);
+    else if (fa == 3) split_fb<3, MODE, NLM, TW, SL>(fb, c, a, smem, row);
+    else if (fa == 2) split_fb<2, MODE, NLM, TW, SL>(fb, c, a, smem, row);
+    else if (fa == 1) split_fb<1, MODE, NLM, TW, SL>(fb, c, a, smem, row);
+    else split_body<0, 1, MODE, NLM, TW, SL>(c, a, smem, row);
 }
 
 #ifdef RAFTCORR_DEV

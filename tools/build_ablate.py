@@ -5,7 +5,8 @@
 Variants: 'exact' (rc::build_f32_ring_kernel, RC_BUILD_EXACT_F32) and the
 split-bf16 kernel (rc::build_split_kernel) under the dev library's
 RAFTCORR_SPLIT_MODE ablation flags: 0 product, 1 no operand loads, 2 no
-epilogue stores, 4 no MFMAs (sums combine; timing only, wrong values).
+epilogue stores, 4 no MFMAs (sums combine; timing only, wrong values); a
+variant NAME=VALUE sets that dev knob instead (e.g. RAFTCORR_SPLIT_RING=85).
 Prints the median / min microseconds per launch of each variant.
 """
 import argparse
@@ -48,16 +49,25 @@ def main():
     dev = torch.device("cuda", 0)
     ll = a.config in bench.LOW_LATENCY_CONFIGS
     # RAFTCORR_SPLIT_MODE values of the split kernel (dev library)
-    variants = ["exact"] + [int(m) for m in a.modes.split(",") if m]
+    variants = ["exact"] + [m if "=" in m else int(m) for m in a.modes.split(",") if m]
     res = {str(v): [] for v in variants}
     with torch.no_grad():
         f1, f2, _ = bench.make_inputs(cfg, dev, seed=1)
 
+        knobs = {m.split("=")[0] for m in variants if isinstance(m, str) and "=" in m}
+
         def run(v):
+            for k in knobs:
+                os.environ.pop(k, None)
             if v == "exact":
                 os.environ["RAFTCORR_SPLIT_MODE"] = "0"
                 return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll, exact_f32=True)
-            os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
+            if isinstance(v, str):   # NAME=VALUE: a dev knob over the product mode
+                os.environ["RAFTCORR_SPLIT_MODE"] = "0"
+                k, val = v.split("=")
+                os.environ[k] = val
+            else:
+                os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
             return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
         ref = None
         for v in variants:
@@ -67,7 +77,7 @@ def main():
         # variants with math and stores (no 1/2/4 ablation bits) must
         # reproduce the product bit for bit
         for v in variants:
-            if isinstance(v, int) and v and not (v & 7) and ref is not None:
+            if ((isinstance(v, int) and v and not (v & 7)) or isinstance(v, str) and "=" in v) and ref is not None:
                 got = run(v)().corr_pyramid[:4]
                 res.setdefault("bit_identical", {})[str(v)] = all(
                     bool(torch.equal(x, y)) for x, y in zip(got, ref))
@@ -78,6 +88,8 @@ def main():
                 fn = run(v)
                 res[str(v)] += time_launches(fn, a.per)
         os.environ["RAFTCORR_SPLIT_MODE"] = "0"
+        for k in knobs:
+            os.environ.pop(k, None)
     ident = res.pop("bit_identical", {})
     nerr = res.pop("norm_err_vs_0", {})
     out = {k: {"median_us": statistics.median(x), "min_us": min(x)} for k, x in res.items()}
@@ -89,8 +101,7 @@ def main():
         v["fp32_equiv_tflops"] = flops / (v["median_us"] * 1e-6) / 1e12
     print(json.dumps({"config": a.config, "variants": out,
                       "legend": "exact = fp32 MFMA ring; split modes (build_split_kernel): 0 "
-                                "product, 1 no loads, 2 no stores, 4 no MFMA, 4096 no wave-role "
-                                "rotation (sums combine)"}, indent=1))
+                                "product, 1 no loads, 2 no stores, 4 no MFMA (sums combine); NAME=VALUE a dev knob"}, indent=1))
 
 
 if __name__ == "__main__":
