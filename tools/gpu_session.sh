@@ -57,7 +57,7 @@ if has pmck; then   # kitti build HBM bytes (profiles/traffic.json "kitti")
 fi
 if has prof; then
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace \
-        -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0
+        -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-steps 0 --config4-steps 0
     find "$OUT/prof" -name "*stats*.csv" -exec sh -c 'echo "== $1"; cat "$1"' _ {} \; > "$OUT/kernel_stats.txt" 2>/dev/null
     head -c 3000 "$OUT/kernel_stats.txt"
 fi
@@ -164,7 +164,7 @@ if has calib; then   # FETCH_SIZE / WRITE_SIZE per byte for scattered 64-256 B r
 fi
 if has pmcjson; then   # profiles/pmc.json: three counter passes of bench.py itself per config
     for C in ${PMC_CONFIGS:-sceneflow kitti middlebury realtime}; do
-        BA="--config $C --pmc-calibrate --steps 2 --warmup 1 --no-cpu-baseline --e2e-steps 0"
+        BA="--config $C --pmc-calibrate --steps 2 --warmup 1 --no-cpu-baseline --e2e-steps 0 --config4-steps 0"
         step pmcj_${C}_f 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcj_${C}_f" -o f -- python3 bench.py $BA
         step pmcj_${C}_w 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcj_${C}_w" -o w -- python3 bench.py $BA
         step pmcj_${C}_s 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES \
