@@ -739,9 +739,24 @@ class CorrBlock1D:
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, *, pyramid_dtype=None,
                  lazy_levels=None, shadow=None, channels_last=False, low_latency=False,
-                 grad_shadow=None, exact_f32=False, grad_deferred=None, layout="rows"):
+                 grad_shadow=None, exact_f32=False, grad_deferred=None, layout="rows",
+                 check_finite=False):
         self.num_levels = num_levels
         self.radius = radius
+        # check_finite (opt-in): the split-bf16 default gives NaN
+        # where the reference's fp32 einsum gives +-inf for inf fmap entries
+        # (pinned by tests/test_split_gpu.py); with
+        # check_finite=True one isfinite reduction over both fmaps (a host
+        # sync) sends non-finite inputs to the exact fp32 kernel, with a
+        # warning, so the volume keeps the reference's +-inf entries
+        if (check_finite and not exact_f32 and fmap1.dtype == torch.float32 and
+                fmap2.dtype == torch.float32 and pyramid_dtype in (None, torch.float32)):
+            if not (bool(torch.isfinite(fmap1).all()) and bool(torch.isfinite(fmap2).all())):
+                warnings.warn("CorrBlock1D: non-finite fmap values -- building on the exact fp32 "
+                              "kernel (exact_f32=True) so that +-inf volume entries stay +-inf",
+                              RuntimeWarning, stacklevel=2)
+                exact_f32 = True
+                layout = "rows"      # the disparity-major build is split-bf16 only
         # layout="disparity" (opt-in, RC_LAYOUT_DISPARITY): the
         # stored levels 0 and 2 disparity-major, so a wave's pixels that look
         # at the same disparity read contiguous memory; the same values and

@@ -152,3 +152,26 @@ def test_split_nonfinite_fmaps_pinned():
     assert np.array_equal(ex[np.isinf(ref)], ref[np.isinf(ref)])
     # split default: NaN wherever the reference is non-finite (the pinned difference)
     assert np.isnan(sp[~fin]).all()
+    # CorrBlock1D(check_finite=True): the non-finite fmaps are
+    # detected, a RuntimeWarning names the switch, and the block is the exact
+    # kernel's bit for bit (levels and lookups); finite fmaps keep the split
+    # default (bit for bit the default block)
+    c = torch.zeros(B, 2, H, W)
+    c[:, 0] = torch.arange(W, dtype=torch.float32) - 3.25
+    with torch.no_grad():
+        with pytest.warns(RuntimeWarning, match="non-finite"):
+            chk = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=2, check_finite=True,
+                              layout="disparity")
+        exb = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=2, exact_f32=True)
+        assert chk.layout == "rows"
+        for u, v in zip(chk.corr_pyramid, exb.corr_pyramid):
+            assert torch.equal(u.view(torch.int32), v.view(torch.int32))
+        assert torch.equal(chk(c.to(DEV)).view(torch.int32), exb(c.to(DEV)).view(torch.int32))
+        g1, g2 = torch.randn(B, D, H, W, generator=g), torch.randn(B, D, H, W, generator=g)
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")
+            fine = CorrBlock1D(g1.to(DEV), g2.to(DEV), num_levels=2, check_finite=True)
+        dflt = CorrBlock1D(g1.to(DEV), g2.to(DEV), num_levels=2)
+        for u, v in zip(fine.corr_pyramid, dflt.corr_pyramid):
+            assert torch.equal(u.view(torch.int32), v.view(torch.int32))
