@@ -928,23 +928,27 @@ def main():
     # the line's value with --config middlebury --network
     net_steps = (max(args.steps, 1) if args.network else
                  args.config4_steps if args.config == "sceneflow" and not proj else 0)
-    if net_steps > 0:
-        leg = row_sharded_network(device, rank, world, net_steps, 1 if not args.network
-                                  else max(args.warmup, 1))
-        if args.network:
-            result["corr_path"] = {k: result[k] for k in ("value", "ms_per_step", "config")}
-            result.update({
-                "value": leg["pairs_per_s"], "ms_per_step": leg["ms_per_pair"],
-                "steps": net_steps, "warmup": leg["warmup"], "scaling": "strong",
-                "network": leg,
-                "config": {"workload": "BASELINE configs[3]: full RAFTStereo network, one "
-                                       "1984x2880 pair, 32 iterations, fp32, image rows sharded "
-                                       f"over {world} rank(s) (encoders with per-module halos, "
-                                       "corr path on own rows, GRU per-conv halo exchange)",
-                           "config": "middlebury", "global_batch": 1, "image": [1984, 2880],
-                           "iters": 32, "parallelism": f"row-shard x{world}"}})
-        else:
-            result["config4_network"] = leg
+    if net_steps > 0 and not args.network:
+        # the side leg must not take the corr-path line down with it: an error
+        # (e.g. from RCCL, which raises on every rank alike) is recorded in
+        # the line instead
+        try:
+            result["config4_network"] = row_sharded_network(device, rank, world, net_steps, 1)
+        except Exception as e:  # noqa: BLE001
+            result["config4_network"] = {"error": f"{type(e).__name__}: {e}"[:600]}
+    elif net_steps > 0:
+        leg = row_sharded_network(device, rank, world, net_steps, max(args.warmup, 1))
+        result["corr_path"] = {k: result[k] for k in ("value", "ms_per_step", "config")}
+        result.update({
+            "value": leg["pairs_per_s"], "ms_per_step": leg["ms_per_pair"],
+            "steps": net_steps, "warmup": leg["warmup"], "scaling": "strong",
+            "network": leg,
+            "config": {"workload": "BASELINE configs[3]: full RAFTStereo network, one "
+                                   "1984x2880 pair, 32 iterations, fp32, image rows sharded "
+                                   f"over {world} rank(s) (encoders with per-module halos, "
+                                   "corr path on own rows, GRU per-conv halo exchange)",
+                       "config": "middlebury", "global_batch": 1, "image": [1984, 2880],
+                       "iters": 32, "parallelism": f"row-shard x{world}"}})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds,
                                               full=args.config == "sceneflow")
