@@ -144,6 +144,46 @@ def test_config1_disparity_matches_reference(name, fuse):
     assert mae <= MAE_PX, mae
 
 
+@pytest.mark.parametrize("name", [n for n in sorted(SEEDED) if SEEDED[n]["W"] == 720])
+def test_config1_disparity_layout_network(name):
+    """CorrBlock1D(layout="disparity") as the network's corr block (the
+    RC_LAYOUT_DISPARITY option), on BASELINE configs[0]: at
+    every iteration its lookup equals the row layout's bit for bit on the
+    network's own coordinates (both blocks built from the same fmaps), its
+    corr_pyramid equals the row layout's, and the final disparity meets the
+    reference golden's 0.01 px bar.  (Two separate network runs are not
+    compared bitwise: MIOpen may pick different convolution algorithms.)"""
+    from golden_util import image_digest, stereo_pair
+    case = SEEDED[name]
+    z = load(f"{GOLDEN}/e2e_{name.split('_', 1)[1]}.npz")
+    img1, img2 = stereo_pair(1, case["H"], case["W"], case["seed"])
+    assert image_digest(img1, img2) == case["image_sha256"]
+    calls = []
+
+    class Checked:
+        def __init__(self, f1, f2, radius, num_levels):
+            self.d = CorrBlock1D(f1, f2, radius=radius, num_levels=num_levels, layout="disparity")
+            self.r = CorrBlock1D(f1, f2, radius=radius, num_levels=num_levels)
+            assert self.d.layout == "disparity"
+            for a, b in zip(self.d.corr_pyramid, self.r.corr_pyramid):
+                assert torch.equal(a.contiguous().view(torch.int32), b.contiguous().view(torch.int32))
+
+        def __call__(self, coords):
+            out = self.d(coords)
+            assert torch.equal(out.view(torch.int32), self.r(coords).view(torch.int32))
+            calls.append(1)
+            return out
+
+    torch.manual_seed(0)
+    model = RAFTStereo(StereoArgs(**case["args"]), corr_block=Checked).eval().cuda()
+    with torch.no_grad():
+        flows = model(img1.cuda(), img2.cuda(), iters=case["iters"])
+    assert len(calls) == case["iters"]
+    disp = flows[-1][:, 0].cpu().numpy()
+    mae = float(np.abs(disp - z["disparity"]).mean())
+    assert mae <= MAE_PX, mae
+
+
 @pytest.mark.parametrize("name", [n for n in sorted(SEEDED) if SEEDED[n]["W"] == 1242])
 def test_config3_bf16_corr_path_disparity(name):
     """BASELINE configs[2]'s image size (one 1x3x375x1242 pair, 32 iterations,
