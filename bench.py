@@ -475,6 +475,25 @@ def launcher_cmd(gpus, argv, port):
             os.path.abspath(__file__)] + list(argv)
 
 
+def leg_watchdog(result, rank, limit):
+    """Timer for the default line's config-4 side leg: if it fires, rank 0
+    prints the line as measured so far with ``config4_network`` marked timed
+    out, and every rank exits 0 (the corr-path measurement stands)."""
+    import threading
+
+    def fire():
+        if rank == 0:
+            line = dict(result)
+            line["config4_network"] = {"error": f"not finished after {limit:.0f} s (hung exchange?)"}
+            print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os._exit(0)
+    t = threading.Timer(limit, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def row_sharded_network(device, rank, world, steps, warmup, iters=32, image_hw=(1984, 2880)):
     """BASELINE configs[3] end to end: ONE synthetic full-resolution pair,
     RAFTStereo (seeded random-init weights, fp32, eval) row-sharded over the
@@ -573,6 +592,8 @@ def main():
                     help="--config middlebury: the line's value is the row-sharded FULL network "
                          "(BASELINE configs[3]: 1984x2880, 32 iterations, GRU halo exchange) "
                          "instead of the corr path alone")
+    ap.add_argument("--config4-timeout", type=float, default=300.0,
+                    help="seconds the default line waits for its config-4 side leg")
     ap.add_argument("--config4-steps", type=int, default=1,
                     help="default (sceneflow) run: also time the row-sharded config-4 network "
                          "this many steps, after one warm-up (0 = skip)")
@@ -933,11 +954,15 @@ def main():
     if net_steps > 0 and not args.network:
         # the side leg must not take the corr-path line down with it: an error
         # (e.g. from RCCL, which raises on every rank alike) is recorded in
-        # the line instead
+        # the line instead, and a leg that has not finished after
+        # --config4-timeout seconds (a hung exchange) prints the line without
+        # it and ends every rank with status 0
+        dog = leg_watchdog(result, rank, args.config4_timeout)
         try:
             result["config4_network"] = row_sharded_network(device, rank, world, net_steps, 1)
         except Exception as e:  # noqa: BLE001
             result["config4_network"] = {"error": f"{type(e).__name__}: {e}"[:600]}
+        dog.cancel()
     elif net_steps > 0:
         leg = row_sharded_network(device, rank, world, net_steps, max(args.warmup, 1))
         result["corr_path"] = {k: result[k] for k in ("value", "ms_per_step", "config")}

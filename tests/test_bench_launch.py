@@ -47,3 +47,22 @@ def test_network_flag_needs_middlebury():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--network"],
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2 and "middlebury" in p.stderr
+
+
+def test_leg_watchdog_prints_the_line_and_exits_zero():
+    """A config-4 side leg that does not finish (a hung exchange) must not
+    cost the corr-path line: rank 0 prints it with the leg marked, every
+    rank exits 0."""
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "bench.leg_watchdog({'metric': 'm', 'value': 1.5}, %d, 0.5); time.sleep(30); print('late')")
+    for rank in (0, 1):
+        p = subprocess.run([sys.executable, "-c", code % (ROOT, rank)], capture_output=True, text=True,
+                           timeout=120)
+        assert p.returncode == 0, p.stderr
+        assert "late" not in p.stdout
+        if rank == 0:
+            import json
+            line = json.loads(p.stdout.strip().splitlines()[-1])
+            assert line["value"] == 1.5 and "not finished" in line["config4_network"]["error"]
+        else:
+            assert p.stdout.strip() == ""
