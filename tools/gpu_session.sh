@@ -154,7 +154,7 @@ has pdisp && step shear_probe_product 900 python tools/shear_probe.py --product 
 has gfloor && step graph_floor 300 python tools/graph_floor.py
 has train && step train_probe 300 python tools/train_probe.py
 has trainmb && step train_probe_middlebury 300 python tools/train_probe.py --config middlebury --reps 3
-has lprobe2 && step lookup_probe2 600 python tools/lookup_probe.py --only-dev --dev-variants ${LPROBE_VARIANTS:-215} --dev-fields ${LPROBE_FIELDS:-bench,smooth,net} --reps ${LPROBE_REPS:-7}
+has lprobe2 && step lookup_probe2 600 python tools/lookup_probe.py --only-dev --dev-variants ${LPROBE_VARIANTS:-205} --dev-fields ${LPROBE_FIELDS:-bench,smooth,net} --reps ${LPROBE_REPS:-7}
 if has calib; then   # FETCH_SIZE / WRITE_SIZE per byte for scattered 64-256 B rows
     step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o f \
         -- python3 tools/pmc_calib_random.py
