@@ -29,24 +29,27 @@ from raft_stereo_amd import _lib  # noqa: E402
 from raft_stereo_amd import corr as rcorr  # noqa: E402
 
 M0 = -8          # first record's level-1 centre (a multiple of 4)
-REC, REC2 = 64, 26
+# slots -> (G level-1 centres per record, level-2 slots, level-0 slots)
+GEOM = {64: (8, 26, 38), 128: (32, 38, 86)}
 
 
-def records(pyr, P, W0, W2l, NR):
-    """(P, NR, 64) bf16: slots 0..25 level-2 elements 4r + M0/2 - 10 + j,
-    slots 26..63 level-0 elements 16r + 2 M0 - 10 + j (zeros off the row)."""
+def records(pyr, P, W0, W2l, NR, slots):
+    """(P, NR, slots) bf16: slots [0, n2) level-2 elements (G/2) r + M0/2 - 10 + j,
+    slots [n2, n2 + n0) level-0 elements 2 G r + 2 M0 - 10 + j (zeros off the
+    row and in any padding slots)."""
+    G, n2s, n0s = GEOM[slots]
     L0 = pyr[0].reshape(P, -1)[:, :W0]
     L2 = pyr[2].reshape(P, -1)[:, :W2l]
     o0, o2 = -(2 * M0 - 10), -(M0 // 2 - 10)          # row offsets of element 0
-    n0 = 16 * (NR - 1) + 38 + o0
-    n2 = 4 * (NR - 1) + 26 + o2
+    n0 = 2 * G * (NR - 1) + n0s + o0
+    n2 = (G // 2) * (NR - 1) + n2s + o2
     Lp0 = torch.zeros(P, max(n0, o0 + W0), dtype=L0.dtype, device=L0.device)
     Lp0[:, o0:o0 + W0] = L0
     Lp2 = torch.zeros(P, max(n2, o2 + W2l), dtype=L2.dtype, device=L2.device)
     Lp2[:, o2:o2 + W2l] = L2
-    rec = torch.empty(P, NR, REC, dtype=L0.dtype, device=L0.device)
-    rec[:, :, REC2:] = Lp0.as_strided((P, NR, REC - REC2), (Lp0.stride(0), 16, 1))
-    rec[:, :, :REC2] = Lp2.as_strided((P, NR, REC2), (Lp2.stride(0), 4, 1))
+    rec = torch.zeros(P, NR, slots, dtype=L0.dtype, device=L0.device)
+    rec[:, :, n2s:n2s + n0s] = Lp0.as_strided((P, NR, n0s), (Lp0.stride(0), 2 * G, 1))
+    rec[:, :, :n2s] = Lp2.as_strided((P, NR, n2s), (Lp2.stride(0), G // 2, 1))
     del Lp0, Lp2
     return rec
 
@@ -56,6 +59,7 @@ def main():
     ap.add_argument("--config", default="kitti")
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--slots", default="64,128", help="record sizes to time (bf16 elements: 64 or 128)")
     a = ap.parse_args()
     B, D, H, W1, W2, L, r, iters, _ = bench.CONFIGS[a.config]
     B = a.batch or B
@@ -64,29 +68,33 @@ def main():
     fn = lib.rc_dev_lookup_records
     fn.restype = ctypes.c_int
     vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
-    fn.argtypes = [vp, ci, ci, ctypes.POINTER(ci), vp, cl, ci, ci, ci, vp, vp]
+    fn.argtypes = [vp, ci, ci, ci, ctypes.POINTER(ci), vp, cl, ci, ci, ci, vp, vp]
     P = B * H * W1
     W1lvl = W2 >> 1
-    NR = (W1lvl + r + 3 - M0) // 8 + 1            # covers m1 up to W_1 + R + 3
+    slot_list = [int(v) for v in a.slots.split(",") if v]
+    NRs = {sl: (W1lvl + r + 3 - M0) // GEOM[sl][0] + 1 for sl in slot_list}   # cover m1 up to W_1 + R + 3
     dev = torch.device("cuda", 0)
-    res = {"config": a.config, "B": B, "NR": NR, "M0": M0}
+    res = {"config": a.config, "B": B, "NR": NRs, "M0": M0}
     with torch.no_grad():
         cfg = (B, D, H, W1, W2, L, r, iters, None)
         f1, f2, cs = bench.make_inputs(cfg, dev, seed=1, dtype=torch.bfloat16)
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=True)
         pyr = rcorr.build_pyramid(f1, f2, 3, torch.bfloat16, skip=(1,))
-        rec = records(pyr, P, W2, W2 >> 2, NR)
+        recs = {sl: records(pyr, P, W2, W2 >> 2, NRs[sl], sl) for sl in slot_list}
         del pyr
-        res["record_MB"] = rec.numel() * 2 / 1e6
+        res["record_MB"] = {sl: t.numel() * 2 / 1e6 for sl, t in recs.items()}
         res["rows_shadowed_MB"] = sum(2 * t.numel() * 2 for t in (blk._levels[0], blk._levels[2])) / 1e6
         widths = _lib.int_array([W2 >> i for i in range(4)])
         out = torch.empty(B, L * (2 * r + 1), H, W1, device=dev).contiguous(memory_format=torch.channels_last)
         stream = torch.cuda.current_stream().cuda_stream
 
-        def rec_lookup(c):
-            rc = fn(rec.data_ptr(), NR, M0, widths, c.data_ptr(), 2 * H * W1, B, H, W1, out.data_ptr(), stream)
-            assert rc == 0, rc
-            return out
+        def rec_lookup_for(sl):
+            def f(c):
+                rc = fn(recs[sl].data_ptr(), NRs[sl], M0, sl, widths, c.data_ptr(), 2 * H * W1, B, H, W1,
+                        out.data_ptr(), stream)
+                assert rc == 0, rc
+                return out
+            return f
 
         from test_corr_gpu import special_coords
         g = torch.Generator().manual_seed(5)
@@ -97,16 +105,17 @@ def main():
         x[(x.abs() < 1e-30) & (x != 0)] = 0.25
         x.view(-1)[100:400] = torch.linspace(-90, W2 + 90, 300, device=dev)   # both row edges
         checks[-1][:, 0] = x
-        for c in checks:
-            ref = blk(c)
-            got = rec_lookup(c)
-            same = torch.equal(ref.nan_to_num(7.0).view(torch.int32), got.nan_to_num(7.0).view(torch.int32))
-            if not same:
-                d = (ref.nan_to_num(7.0) - got.nan_to_num(7.0)).abs()
-                print("MISMATCH", d.max().item(), int((d > 0).sum()), flush=True)
-            assert same
+        for sl in slot_list:
+            for c in checks:
+                ref = blk(c).clone()
+                got = rec_lookup_for(sl)(c)
+                same = torch.equal(ref.nan_to_num(7.0).view(torch.int32), got.nan_to_num(7.0).view(torch.int32))
+                if not same:
+                    d = (ref.nan_to_num(7.0) - got.nan_to_num(7.0)).abs()
+                    print("MISMATCH", sl, d.max().item(), int((d > 0).sum()), flush=True)
+                assert same
         res["bit_identical"] = True
-        variants = [("product", blk), ("records", rec_lookup)]
+        variants = [("product", blk)] + [(f"records{sl}", rec_lookup_for(sl)) for sl in slot_list]
         per = {n: [] for n, _ in variants}
         for _ in range(a.reps):
             for name, f in variants:
