@@ -81,50 +81,3 @@ def test_levelpar_levels_radius_vs_oracle(shape):
     ref = coracle.corr_lookup([t.cpu().numpy() for t in pyr], c.numpy(), L, r)
     assert np.array_equal(a, ref, equal_nan=True)
     assert np.array_equal(b, ref, equal_nan=True)
-
-
-# Round 5 (measured, not kept: DESIGN.md §3.2g): the level-parallel lookup
-# staging each level's 64 block rows in LDS before reading the coords (dev
-# variant 8, lookup_levelpar_lds_kernel).  Bit for bit the product's unstaged
-# kernel, incl. the fused step, a ragged last block, bf16 rows and a shape
-# whose rows exceed the LDS budget (the variant then defers to the product).
-LDS_SHAPES = [
-    # B, D, H, W1, W2, L, r
-    (1, 32, 3, 160, 160, 3, 4),     # realtime rows (120x160 at full size)
-    (1, 16, 3, 50, 50, 1, 4),       # P = 150: a ragged last block
-    (2, 16, 3, 40, 44, 2, 5),       # W2 % 8 != 0 (bf16 rows not 16-B multiples)
-    (1, 16, 2, 90, 90, 4, 8),
-    (1, 16, 2, 200, 300, 2, 4),     # 64 x (300 + 150) x 4 B > 72 KB: unstaged
-]
-
-
-@pytest.mark.parametrize("shape", LDS_SHAPES, ids=lambda s: "x".join(map(str, s)))
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-def test_levelpar_lds_matches_unstaged(shape, dt):
-    import os
-    from raft_stereo_amd import _lib
-    B, D, H, W1, W2, L, r = shape
-    if dt == torch.bfloat16 and L not in (2, 4):
-        pytest.skip("bf16 pyramids: 2 or 4 levels")
-    g = torch.Generator().manual_seed(4400 + sum(shape))
-    f1 = torch.randn(B, D, H, W1, generator=g).to(DEV)
-    f2 = torch.randn(B, D, H, W2, generator=g).to(DEV)
-    coords = special_coords(B, H, W1, W2, g).to(DEV)
-    d = torch.randn(coords.shape, generator=g).to(DEV)
-    with torch.no_grad():
-        blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, pyramid_dtype=dt, low_latency=True)
-        out = blk(coords)
-        c1 = coords.clone()
-        st = blk.lookup_step(c1, d, out=c1)
-        with _lib.dev_library():
-            os.environ["RAFTCORR_LOOKUP_VARIANT"] = "8"
-            try:
-                ref = blk(coords)
-                c2 = coords.clone()
-                st2 = blk.lookup_step(c2, d, out=c2)
-            finally:
-                os.environ["RAFTCORR_LOOKUP_VARIANT"] = "0"
-    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
-    for u, v in zip(st, st2):
-        assert torch.equal(u.view(torch.int32), v.view(torch.int32))
-    assert torch.equal(c1.view(torch.int32), c2.view(torch.int32))
