@@ -13,6 +13,7 @@ strictly row-local -- row h of fmap1 only meets row h of fmap2
 again with no exchange.  ``RowShardedStereo`` runs the whole network that
 way, exchanging only the GRU state halos each iteration.
 """
+import contextlib
 import time
 
 import torch
@@ -307,7 +308,7 @@ class RowShardedStereo:
     """
 
     def __init__(self, model, rank, world, halo=None, group=None, shard_encoders=True, enc_margin=48,
-                 per_stage=True, encoder_halos=True, overlap=True, per_conv=None):
+                 per_stage=True, encoder_halos=True, overlap=True, per_conv=None, side_stream=True):
         # per_conv (the default unless a slab ``halo`` or per_stage=False is
         # asked for): GRU state on own rows, each conv evaluated on the rows its
         # readers need, halos exchanged per update (_forward_perconv)
@@ -340,6 +341,12 @@ class RowShardedStereo:
         # (RCCL: on the comm stream).  Same ops on the same values: the result
         # equals the blocking order bit for bit.
         self.overlap = overlap
+        # side_stream (per-conv mode, HIP tensors): each iteration's corr
+        # lookup + motion encoder run on a second stream while the coarser
+        # GRUs run on the current one -- two independent chains of small
+        # kernels whose fixed per-launch cost dominates at 60-row slabs
+        # (DESIGN.md §5); same ops on the same values, bit for bit
+        self.side_stream = side_stream
         self._fake_xchg = False     # tools/shard_probe.py: time one rank's compute alone
         self.xchg_wait_s = 0.0      # host time spent blocked in exchange waits
         self.xchg_count = 0
@@ -834,7 +841,14 @@ class RowShardedStereo:
         lo0, hi0 = own[0]
         fh = blk.flow_head
         p2 = fh.conv2.padding[0]
-        for _ in range(iters):
+        dev = netS[0].t.device
+        side = torch.cuda.Stream(dev) if self.side_stream and dev.type == "cuda" else None
+        # with the side stream and the default GRU schedule, gru32 of the next
+        # iteration (its inputs: this iteration's net1 and net2) runs on the
+        # side stream while gru08 and the flow head run on this one
+        ahead = side is not None and n == 3 and not a.slow_fast_gru
+        e32 = None
+        for it in range(iters):
             with m._autocast():
                 if n == 3 and a.slow_fast_gru:
                     gru32()
@@ -842,15 +856,34 @@ class RowShardedStereo:
                     if n == 3:
                         gru32()
                     gru16()
-                if n == 3:
+                if n == 3 and e32 is None:
                     gru32()
+            if e32 is not None:
+                torch.cuda.current_stream(dev).wait_event(e32)
+                e32 = None
             cS = get("coords")
-            corr = _Rows(corr_fn(cS.rows(c0, c1).contiguous()), c0, H1)
-            flow = _Rows(cS.t - coords0, k0, H1)
+            main = torch.cuda.current_stream(dev) if side is not None else None
+            if side is not None:      # the motion chain on the side stream, gru16 on this one
+                side.wait_stream(main)
+            with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+                corr = _Rows(corr_fn(cS.rows(c0, c1).contiguous()), c0, H1)
+                flow = _Rows(cS.t - coords0, k0, H1)
+                with m._autocast():
+                    motion = _motion_rows(blk.encoder, corr, flow, lo0 - gp[0], hi0 + gp[0])
             with m._autocast():
-                motion = _motion_rows(blk.encoder, corr, flow, lo0 - gp[0], hi0 + gp[0])
                 if n >= 2:
                     gru16()
+                if side is not None:
+                    main.wait_stream(side)
+                    motion.t.record_stream(main)      # made on the side stream, read here
+                if ahead and it + 1 < iters:
+                    # net1's exchange completes on this stream first, so that
+                    # both streams are ordered after it
+                    get("net1")
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        gru32()
+                        e32 = side.record_event()
                 xs = [motion]
                 if n > 1:
                     xs.append(_interp_rows_held(get("net1"), lo0 - gp[0], hi0 + gp[0], glob[0],
