@@ -843,52 +843,27 @@ class RowShardedStereo:
         p2 = fh.conv2.padding[0]
         dev = netS[0].t.device
         side = torch.cuda.Stream(dev) if self.side_stream and dev.type == "cuda" else None
-        # with the side stream and the default GRU schedule, gru32 of the next
-        # iteration (its inputs: this iteration's net1 and net2) runs on the
-        # side stream while gru08 and the flow head run on this one
-        ahead = side is not None and n == 3 and not a.slow_fast_gru
-        e32 = None
-        for it in range(iters):
-            with m._autocast():
-                if n == 3 and a.slow_fast_gru:
-                    gru32()
-                if n >= 2 and a.slow_fast_gru:
-                    if n == 3:
-                        gru32()
-                    gru16()
-                if n == 3 and e32 is None:
-                    gru32()
-            if e32 is not None:
-                torch.cuda.current_stream(dev).wait_event(e32)
-                e32 = None
+
+        def motion_chain():
+            """corr lookup + motion encoder of this iteration (current stream)."""
             cS = get("coords")
-            main = torch.cuda.current_stream(dev) if side is not None else None
-            if side is not None:      # the motion chain on the side stream, gru16 on this one
-                side.wait_stream(main)
-            with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
-                corr = _Rows(corr_fn(cS.rows(c0, c1).contiguous()), c0, H1)
-                flow = _Rows(cS.t - coords0, k0, H1)
-                with m._autocast():
-                    motion = _motion_rows(blk.encoder, corr, flow, lo0 - gp[0], hi0 + gp[0])
+            corr = _Rows(corr_fn(cS.rows(c0, c1).contiguous()), c0, H1)
+            flow = _Rows(cS.t - coords0, k0, H1)
             with m._autocast():
-                if n >= 2:
-                    gru16()
-                if side is not None:
-                    main.wait_stream(side)
-                    motion.t.record_stream(main)      # made on the side stream, read here
-                if ahead and it + 1 < iters:
-                    # net1's exchange completes on this stream first, so that
-                    # both streams are ordered after it
-                    get("net1")
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        gru32()
-                        e32 = side.record_event()
+                motion = _motion_rows(blk.encoder, corr, flow, lo0 - gp[0], hi0 + gp[0])
+            return cS, motion
+
+        def gru08(motion):
+            with m._autocast():
                 xs = [motion]
                 if n > 1:
                     xs.append(_interp_rows_held(get("net1"), lo0 - gp[0], hi0 + gp[0], glob[0],
                                                 widths[0]))
                 gru(0, xs)
+
+        def flow_head(cS):
+            """flow head, coords update and its exchange (current stream)."""
+            with m._autocast():
                 hid = _relu(_conv_rows(fh.conv1, get("net0"), lo0 - p2, hi0 + p2))
                 delta = _conv_rows(fh.conv2, hid, lo0, hi0).t
             delta = delta.float()
@@ -896,6 +871,78 @@ class RowShardedStereo:
             c_own = cS.rows(lo0, hi0) + delta
             preds.append(c_own - grid[:, :, lo0:hi0])
             post("coords", c_own, 0, hc)
+
+        if side is not None and n == 3 and not a.slow_fast_gru:
+            # the default schedule as a two-stream pipeline: this stream runs
+            # gru16 and gru08; the side stream runs the corr lookup + motion
+            # encoder, the next iteration's gru32 (inputs: this iteration's
+            # net1 and net2) and the flow head + coords update (input: gru08's
+            # net0), each behind the event of what it reads.  Every exchange
+            # a stream reads is completed (get) on this stream before the side
+            # stream is ordered after it; tensors made on the side stream and
+            # read here are record_stream-ed.
+            main = torch.cuda.current_stream(dev)
+            with m._autocast():
+                gru32()
+            get("coords")
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                cS, motion = motion_chain()
+            e32 = None
+            for it in range(iters):
+                if e32 is not None:
+                    main.wait_event(e32)
+                with m._autocast():
+                    gru16()
+                main.wait_stream(side)
+                motion.t.record_stream(main)
+                last = it + 1 == iters
+                if not last:
+                    get("net1")
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        with m._autocast():
+                            gru32()
+                        e32 = side.record_event()
+                gru08(motion)
+                get("net0")
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    flow_head(cS)
+                    if not last:
+                        cS, motion = motion_chain()
+            main.wait_stream(side)
+            for p_ in preds:
+                p_.record_stream(main)
+        else:
+            for _ in range(iters):
+                with m._autocast():
+                    if n == 3 and a.slow_fast_gru:
+                        gru32()
+                    if n >= 2 and a.slow_fast_gru:
+                        if n == 3:
+                            gru32()
+                        gru16()
+                    if n == 3:
+                        gru32()
+                if side is not None:      # the motion chain on the side stream, gru16 on this one
+                    main = torch.cuda.current_stream(dev)
+                    get("coords")
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        cS, motion = motion_chain()
+                    with m._autocast():
+                        if n >= 2:
+                            gru16()
+                    main.wait_stream(side)
+                    motion.t.record_stream(main)
+                else:
+                    cS, motion = motion_chain()
+                    with m._autocast():
+                        if n >= 2:
+                            gru16()
+                gru08(motion)
+                flow_head(cS)
         for key in list(state):         # drain the last iteration's exchanges
             get(key)
         return preds
