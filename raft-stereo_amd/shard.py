@@ -842,7 +842,11 @@ class RowShardedStereo:
         fh = blk.flow_head
         p2 = fh.conv2.padding[0]
         dev = netS[0].t.device
-        side = torch.cuda.Stream(dev) if self.side_stream and dev.type == "cuda" else None
+        side = None
+        if self.side_stream and dev.type == "cuda":      # one side stream per instance and device
+            if getattr(self, "_side", None) is None or self._side.device != dev:
+                self._side = torch.cuda.Stream(dev)
+            side = self._side
 
         def motion_chain():
             """corr lookup + motion encoder of this iteration (current stream)."""
