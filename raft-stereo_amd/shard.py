@@ -139,6 +139,16 @@ class _Rows:
         return F.pad(self.t[:, :, s0 - self.g0:s1 - self.g0], (0, 0, s0 - lo, hi - s1))
 
 
+class _Conv:
+    """weight / bias with another conv's geometry (padding, stride, dilation,
+    groups), for _conv_rows."""
+    __slots__ = ("weight", "bias", "padding", "stride", "dilation", "groups")
+
+    def __init__(self, weight, bias, like):
+        self.weight, self.bias = weight, bias
+        self.padding, self.stride, self.dilation, self.groups = like.padding, like.stride, like.dilation, like.groups
+
+
 def _conv_rows(conv, x, lo, hi):
     """``conv`` (stride 1, zero 'same' padding) evaluated on output rows
     [lo, hi) only, clipped to the level: the full-image op's values on those
@@ -208,18 +218,46 @@ def _cat_rows(parts, lo, hi):
     return _Rows(torch.cat([p.rows(s0, s1) for p in parts], 1), s0, parts[0].H)
 
 
-def _gru_rows(gru, h, cz, cr, cq, xs, lo, hi):
+_ZR = {}     # id(ConvGRU) -> (weight, bias, C, tag): convz and convr stacked along the output channels
+
+
+def _zr_conv(gru):
+    """convz and convr as ONE conv (weights stacked along the output channels):
+    the same per-channel sums, one launch instead of two and no sliced input
+    for convz -- at 60-row slabs each launch's fixed cost matters (DESIGN.md
+    §5).  Cached per module; rebuilt if its weights are replaced."""
+    k = id(gru)
+    wz, wr = gru.convz.weight, gru.convr.weight
+    bz, br = gru.convz.bias, gru.convr.bias
+    # the tensors AND their in-place versions (load_state_dict copies in place)
+    tag = tuple((id(t), t._version) for t in (wz, wr, bz, br) if t is not None)
+    hit = _ZR.get(k)
+    if hit is None or hit[3] != tag:
+        w = torch.cat([wz, wr], 0)
+        b = None if bz is None else torch.cat([bz, br], 0)
+        hit = _ZR[k] = (w, b, wz.shape[0], tag)
+    return hit[0], hit[1], hit[2]
+
+
+def _gru_rows(gru, h, cz, cr, cq, xs, lo, hi, fuse_zr=True):
     """ConvGRU.forward (model.py:164-179) on output rows [lo, hi): z on
     [lo, hi), r on the rows convq reads, both from [h, x] on one more cone
     of rows; r*h and x zero outside the image as the full op pads them.
     ``h``, ``cz``, ``cr``, ``cq`` and each of ``xs`` are _Rows holding
-    enough rows.  Returns the new hidden state's rows [lo, hi)."""
+    enough rows.  ``fuse_zr``: convz and convr as one stacked conv over r's
+    rows (z's rows cut from it).  Returns the new hidden state's rows [lo, hi)."""
     H = h.H
     p, pq = gru.convz.padding[0], gru.convq.padding[0]
     ra, rb = max(lo - pq, 0), min(hi + pq, H)                 # rows of r (convq's input)
     hx = _cat_rows([h] + list(xs), ra - p, rb + p)
-    z = torch.sigmoid(_conv_rows(gru.convz, hx, lo, hi).t + cz.rows(lo, hi))
-    r = torch.sigmoid(_conv_rows(gru.convr, hx, ra, rb).t + cr.rows(ra, rb))
+    if fuse_zr and gru.convz.padding == gru.convr.padding and gru.convz.kernel_size == gru.convr.kernel_size:
+        w, b, C = _zr_conv(gru)
+        zr = _conv_rows(_Conv(w, b, gru.convz), hx, ra, rb).t
+        z = torch.sigmoid(zr[:, :C, lo - ra:hi - ra] + cz.rows(lo, hi))
+        r = torch.sigmoid(zr[:, C:] + cr.rows(ra, rb))
+    else:
+        z = torch.sigmoid(_conv_rows(gru.convz, hx, lo, hi).t + cz.rows(lo, hi))
+        r = torch.sigmoid(_conv_rows(gru.convr, hx, ra, rb).t + cr.rows(ra, rb))
     rx = _cat_rows([_Rows(r * h.rows(ra, rb), ra, H)] + list(xs), ra, rb)
     q = torch.tanh(_conv_rows(gru.convq, rx, lo, hi).t + cq.rows(lo, hi))
     return (1 - z) * h.rows(lo, hi) + z * q
@@ -308,7 +346,8 @@ class RowShardedStereo:
     """
 
     def __init__(self, model, rank, world, halo=None, group=None, shard_encoders=True, enc_margin=48,
-                 per_stage=True, encoder_halos=True, overlap=True, per_conv=None, side_stream=True):
+                 per_stage=True, encoder_halos=True, overlap=True, per_conv=None, side_stream=True,
+                 fuse_zr=True):
         # per_conv (the default unless a slab ``halo`` or per_stage=False is
         # asked for): GRU state on own rows, each conv evaluated on the rows its
         # readers need, halos exchanged per update (_forward_perconv)
@@ -347,6 +386,9 @@ class RowShardedStereo:
         # kernels whose fixed per-launch cost dominates at 60-row slabs
         # (DESIGN.md §5); same ops on the same values, bit for bit
         self.side_stream = side_stream
+        # fuse_zr (per-conv mode): each ConvGRU's convz and convr as one conv
+        # with stacked weights (_zr_conv): one launch instead of two
+        self.fuse_zr = fuse_zr
         self._fake_xchg = False     # tools/shard_probe.py: time one rank's compute alone
         self.xchg_wait_s = 0.0      # host time spent blocked in exchange waits
         self.xchg_count = 0
@@ -823,7 +865,7 @@ class RowShardedStereo:
         def gru(l, xs):
             g = (blk.gru08, blk.gru16, blk.gru32)[l]
             lo, hi = own[l]
-            h = _gru_rows(g, get(f"net{l}"), *inpS[l], xs, lo, hi)
+            h = _gru_rows(g, get(f"net{l}"), *inpS[l], xs, lo, hi, fuse_zr=self.fuse_zr)
             post(f"net{l}", h, l, hz["net"][l])
 
         def gru32():

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--W", type=int, default=2880)
     ap.add_argument("--only", type=int, default=0, help="one N only (e.g. under rocprofv3)")
     ap.add_argument("--no-side", action="store_true", help="RowShardedStereo(side_stream=False)")
+    ap.add_argument("--no-fuse", action="store_true", help="RowShardedStereo(fuse_zr=False)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -40,7 +41,7 @@ def main():
     out = {}
     with torch.no_grad():
         for N in ((a.only,) if a.only else (1, 2, 4, 8)):
-            rs = RowShardedStereo(model, N // 2, N, side_stream=not a.no_side)
+            rs = RowShardedStereo(model, N // 2, N, side_stream=not a.no_side, fuse_zr=not a.no_fuse)
             rs._fake_xchg = True
             acc = {"encoders": 0.0, "corr_build": 0.0}
             st0, cb0 = rs._perconv_state, model.corr_block
