@@ -88,23 +88,40 @@ class RowShardedCorr:
 # Row-sharded network forward (BASELINE config 4: full-resolution, bs=1)
 # ---------------------------------------------------------------------------
 
+_INTERP = {}   # row geometry -> (l0, l1, lam): the same every iteration
+
+
+def _interp_index(src_lo, src_glob, dst_lo, dst_hi, dst_glob, hs, device):
+    """The global row mapping of _interp_rows (source rows l0, l1 inside the
+    slab and the weight lam of each destination row), computed once per
+    geometry and device: the GRU loop asks for the same few every iteration,
+    and each recomputation is a dozen tiny kernels."""
+    key = (src_lo, src_glob, dst_lo, dst_hi, dst_glob, hs, str(device))
+    hit = _INTERP.get(key)
+    if hit is None:
+        if len(_INTERP) > 256:
+            _INTERP.clear()
+        scale = (src_glob - 1) / (dst_glob - 1) if dst_glob > 1 else 0.0
+        i = torch.arange(dst_lo, dst_hi, device=device, dtype=torch.float32)
+        pos = (i * scale).clamp(max=src_glob - 1)
+        h0 = pos.floor()
+        lam = (pos - h0).view(1, 1, -1, 1)
+        h0 = h0.long()
+        h1 = torch.clamp(h0 + 1, max=src_glob - 1)
+        l0 = (h0 - src_lo).clamp(0, hs - 1)
+        l1 = (h1 - src_lo).clamp(0, hs - 1)
+        hit = _INTERP[key] = (l0, l1, lam, 1 - lam)
+    return hit
+
+
 def _interp_rows(x, src_lo, src_glob, dst_lo, dst_hi, dst_glob, dst_w):
     """bilinear, align_corners=True resize of a row SLAB (model.py:184-186)
     with the GLOBAL row mapping: destination rows [dst_lo, dst_hi) of a level
     of height dst_glob, from source rows [src_lo, src_lo + x.shape[2]) of a
     level of height src_glob.  Source rows outside the slab are clamped (only
     halo rows can need them; the halo absorbs the error)."""
-    scale = (src_glob - 1) / (dst_glob - 1) if dst_glob > 1 else 0.0
-    i = torch.arange(dst_lo, dst_hi, device=x.device, dtype=torch.float32)
-    pos = (i * scale).clamp(max=src_glob - 1)
-    h0 = pos.floor()
-    lam = (pos - h0).view(1, 1, -1, 1)
-    h0 = h0.long()
-    h1 = torch.clamp(h0 + 1, max=src_glob - 1)
-    hs = x.shape[2]
-    l0 = (h0 - src_lo).clamp(0, hs - 1)
-    l1 = (h1 - src_lo).clamp(0, hs - 1)
-    rows = x[:, :, l0] * (1 - lam) + x[:, :, l1] * lam
+    l0, l1, lam, one_m_lam = _interp_index(src_lo, src_glob, dst_lo, dst_hi, dst_glob, x.shape[2], x.device)
+    rows = x[:, :, l0] * one_m_lam + x[:, :, l1] * lam      # fp32 weights, promoted as before
     return torch.nn.functional.interpolate(rows, (dst_hi - dst_lo, dst_w), mode="bilinear",
                                            align_corners=True)
 
