@@ -15,6 +15,7 @@ way, exchanging only the GRU state halos each iteration.
 """
 import contextlib
 import time
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -235,7 +236,7 @@ def _cat_rows(parts, lo, hi):
     return _Rows(torch.cat([p.rows(s0, s1) for p in parts], 1), s0, parts[0].H)
 
 
-_ZR = {}     # id(ConvGRU) -> (weight, bias, C, tag): convz and convr stacked along the output channels
+_ZR = weakref.WeakKeyDictionary()   # ConvGRU -> (weight, bias, C, tag): convz and convr stacked
 
 
 def _zr_conv(gru):
@@ -243,16 +244,15 @@ def _zr_conv(gru):
     the same per-channel sums, one launch instead of two and no sliced input
     for convz -- at 60-row slabs each launch's fixed cost matters (DESIGN.md
     §5).  Cached per module; rebuilt if its weights are replaced."""
-    k = id(gru)
     wz, wr = gru.convz.weight, gru.convr.weight
     bz, br = gru.convz.bias, gru.convr.bias
     # the tensors AND their in-place versions (load_state_dict copies in place)
     tag = tuple((id(t), t._version) for t in (wz, wr, bz, br) if t is not None)
-    hit = _ZR.get(k)
+    hit = _ZR.get(gru)
     if hit is None or hit[3] != tag:
         w = torch.cat([wz, wr], 0)
         b = None if bz is None else torch.cat([bz, br], 0)
-        hit = _ZR[k] = (w, b, wz.shape[0], tag)
+        hit = _ZR[gru] = (w, b, wz.shape[0], tag)
     return hit[0], hit[1], hit[2]
 
 
