@@ -485,6 +485,7 @@ def leg_watchdog(result, rank, limit):
         if rank == 0:
             line = dict(result)
             line["config4_network"] = {"error": f"not finished after {limit:.0f} s (hung exchange?)"}
+            line["status"] = "config4_leg_timeout"
             print(json.dumps(line), flush=True)
         sys.stdout.flush()
         os._exit(0)
@@ -533,14 +534,31 @@ def row_sharded_network(device, rank, world, steps, warmup, iters=32, image_hw=(
     hz = rs.perconv_halos()
     r0, r1 = rs._own_rows(RowShardedStereo._heights(H, model.args.n_downsample,
                                                     model.args.n_gru_layers), hz)
+    flow_rows = int(preds[-1].shape[2])
+    unsharded = None
+    if world == 1:
+        # the plain RAFTStereo on the same pair: the N=1 baseline every
+        # N-rank speedup is computed against is the faster of the two
+        # 
+        del preds
+        with torch.no_grad():
+            model(img1, img2, iters=iters)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                model(img1, img2, iters=iters)
+            torch.cuda.synchronize()
+        unsharded = (time.perf_counter() - t0) / steps * 1e3
     return {"pairs_per_s": 1.0 / sec, "ms_per_pair": sec * 1e3, "world": world,
+            "unsharded_ms_per_pair": unsharded,
+            "n1_baseline_ms_per_pair": None if unsharded is None else min(unsharded, sec * 1e3),
             "image": [H, W], "iters": iters, "steps": steps, "warmup": warmup,
             "rank0_own_rows": [r0, r1], "halos": {k: hz[k] for k in ("net", "inp", "fmap", "coords")},
             "rank0_exchanges_per_pair": rs.xchg_count / steps,
             "rank0_recv_mb_per_pair": rs.xchg_bytes / steps / 1e6,
             "rank0_wait_ms_per_pair": rs.xchg_wait_s / steps * 1e3,
             "rank0_own_time_ms": own / steps * 1e3,
-            "flow_rows": int(preds[-1].shape[2]),
+            "flow_rows": flow_rows,
             "backend": dist.get_backend() if world > 1 else None,
             "note": "full network (encoders/GRU/heads on PyTorch ops, corr path on the HIP "
                     "kernels), one 1984x2880 pair row-sharded over the ranks; halo exchanges "

@@ -96,8 +96,12 @@ def _interp_index(src_lo, src_glob, dst_lo, dst_hi, dst_glob, hs, device):
     """The global row mapping of _interp_rows (source rows l0, l1 inside the
     slab and the weight lam of each destination row), computed once per
     geometry and device: the GRU loop asks for the same few every iteration,
-    and each recomputation is a dozen tiny kernels."""
-    key = (src_lo, src_glob, dst_lo, dst_hi, dst_glob, hs, str(device))
+    and each recomputation is a dozen tiny kernels.  The key
+    holds the current HIP stream: an entry is built and read on one stream
+    only, so no reader can see it before its kernels finish and clear()
+    frees nothing another stream still has queued."""
+    sid = torch.cuda.current_stream(device).stream_id if device.type == "cuda" else 0
+    key = (src_lo, src_glob, dst_lo, dst_hi, dst_glob, hs, str(device), sid)
     hit = _INTERP.get(key)
     if hit is None:
         if len(_INTERP) > 256:
@@ -243,11 +247,18 @@ def _zr_conv(gru):
     """convz and convr as ONE conv (weights stacked along the output channels):
     the same per-channel sums, one launch instead of two and no sliced input
     for convz -- at 60-row slabs each launch's fixed cost matters (DESIGN.md
-    §5).  Cached per module; rebuilt if its weights are replaced."""
+    §5).  Cached per module only while no gradient is recorded (a cached
+    autograd node could not be back-propagated twice); the cache entry is
+    keyed on each weight's storage, in-place version, dtype and device, so
+    ``.to()`` / ``.double()`` / ``load_state_dict`` (which keep the Parameter
+    object) rebuild it."""
     wz, wr = gru.convz.weight, gru.convr.weight
     bz, br = gru.convz.bias, gru.convr.bias
-    # the tensors AND their in-place versions (load_state_dict copies in place)
-    tag = tuple((id(t), t._version) for t in (wz, wr, bz, br) if t is not None)
+    ws = [t for t in (wz, wr, bz, br) if t is not None]
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ws):
+        w = torch.cat([wz, wr], 0)
+        return w, (None if bz is None else torch.cat([bz, br], 0)), wz.shape[0]
+    tag = tuple((t.data_ptr(), t._version, t.dtype, t.device) for t in ws)
     hit = _ZR.get(gru)
     if hit is None or hit[3] != tag:
         w = torch.cat([wz, wr], 0)
@@ -401,7 +412,9 @@ class RowShardedStereo:
         # lookup + motion encoder run on a second stream while the coarser
         # GRUs run on the current one -- two independent chains of small
         # kernels whose fixed per-launch cost dominates at 60-row slabs
-        # (DESIGN.md §5); same ops on the same values, bit for bit
+        # (DESIGN.md §5); the same ops on the same values, so the result
+        # agrees with the one-stream order within MIOpen's run-to-run noise
+        # (measured 2-4e-6 px; tests/test_shard_gpu.py holds it to 1e-4 px)
         self.side_stream = side_stream
         # fuse_zr (per-conv mode): each ConvGRU's convz and convr as one conv
         # with stacked weights (_zr_conv): one launch instead of two

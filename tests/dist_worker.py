@@ -244,3 +244,42 @@ def run_gpu(rank, world, port, q, halo=32, iters=4):
         q.put((rank, traceback.format_exc(), None))
     finally:
         dist.destroy_process_group()
+
+
+def seeded_images(name):
+    """The images of a seeded BASELINE-size golden (make_golden.e2e_seeded_case),
+    regenerated from its seed, with the manifest's sha256 checked."""
+    from golden_util import image_digest, manifest, stereo_pair
+    case = manifest()["cases"][name]
+    img1, img2 = stereo_pair(1, case["H"], case["W"], case["seed"])
+    assert image_digest(img1, img2) == case["image_sha256"], name
+    return img1, img2, case
+
+
+def run_gpu_config4(rank, world, port, q, iters=32):
+    """BASELINE configs[3] row-sharded over ``world`` ranks sharing cuda:0
+    (gloo, host-staged exchanges): the product RowShardedStereo defaults
+    (per-conv halos, side stream, stacked z/r convs) on the 1984x2880 golden
+    pair; rank 0 returns the gathered final disparity."""
+    import torch
+    import torch.distributed as dist
+    import pkgload
+    pkgload.load()
+    from raft_stereo_amd.shard import RowShardedStereo
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = gpu_model()
+        img1, img2, _ = seeded_images("e2e_config4")
+        with torch.no_grad():
+            rs = RowShardedStereo(net, rank, world)
+            assert rs.per_conv and rs.side_stream and rs.fuse_zr
+            preds = rs.forward(img1.cuda(), img2.cuda(), iters=iters)
+            disp = rs.gather_rows(preds[-1])[:, 0].cpu()
+        q.put((rank, disp if rank == 0 else torch.zeros(0), None))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()

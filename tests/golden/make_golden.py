@@ -242,6 +242,11 @@ def main():
         # BASELINE.json configs[2]'s image size: one 1x3x375x1242 pair, 32 iterations
         # (the fp32 reference; the GPU test runs the bf16 corr path against it)
         "e2e_config3": lambda: e2e_seeded_case(ref, "config3", 375, 1242, 32, 103),
+        # BASELINE.json configs[1]'s image size: one 1x3x540x960 pair, 32 iterations
+        "e2e_config2": lambda: e2e_seeded_case(ref, "config2", 540, 960, 32, 102),
+        # BASELINE.json configs[3]: one 1x3x1984x2880 pair, 32 iterations (the
+        # output RowShardedStereo's 1/2/4/8-GPU runs are checked against)
+        "e2e_config4": lambda: e2e_seeded_case(ref, "config4", 1984, 2880, 32, 104),
     }
     for name, make in todo.items():
         if not only or name in only:

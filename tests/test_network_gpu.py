@@ -120,10 +120,12 @@ SEEDED = {k: v for k, v in manifest()["cases"].items() if v["kind"] == "e2e_seed
 
 @pytest.mark.parametrize("fuse", ["none", "step", "convc1"])
 @pytest.mark.parametrize("name", sorted(SEEDED))
-def test_config1_disparity_matches_reference(name, fuse):
-    """BASELINE configs[0]: one 1x3x320x720 pair, 12 iterations, default args,
-    seeded weights (hash checked) -- the HIP corr path inside the network vs
-    the reference's final disparity (model.py:354-383 + the D8 tail), MAE bar
+def test_seeded_disparity_matches_reference(name, fuse):
+    """The BASELINE image sizes, one pair each, default args, seeded weights
+    (hash checked): configs[0] (320x720, 12 iterations), configs[1]
+    (540x960, 32), configs[2]'s image (375x1242, 32) and configs[3]
+    (1984x2880, 32) -- the HIP corr path inside the network vs the
+    reference's final disparity (model.py:354-383 + the D8 tail), MAE bar
     0.01 px.  Images are regenerated from the seed and their sha256 checked."""
     from golden_util import image_digest, stereo_pair
     case = SEEDED[name]

@@ -183,6 +183,40 @@ def test_gloo_perconv_row_sharded_network(world, H, W, shard_enc, enc_halos, slo
         assert (got - ref).abs().mean() < 1e-6
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_gloo_perconv_row_sharded_config4_geometry(world):
+    """config 4's ROW geometry (1984 image rows -> 496 /
+    248 / 124 feature rows) at world 4 and 8, narrow (64 columns) so the CPU
+    can run it.  At world 8 each rank owns 60-64 rows at 1/4 res and 15-16 at
+    1/16 res against net halos of [5, 5, 2] rows, so every GRU level's halo
+    reaches across a whole neighbour-adjacent band -- the edge-to-edge
+    bookkeeping the 8-GPU run relies on.  Per-conv default (own rows,
+    encoders with per-module halos, overlapped exchanges) == the unsharded
+    network at the fp32 bars of test_gloo_perconv_row_sharded_network."""
+    H, W, iters = 1984, 64, 2
+    res = _spawn(dist_worker.run_rows, world, None, H, W, iters, True, True, True, False, True,
+                 True, None)
+    g = torch.Generator().manual_seed(3)
+    img1 = torch.rand(1, 3, H, W, generator=g) * 255
+    img2 = torch.roll(img1, -4, dims=-1)
+    with torch.no_grad():
+        ref = torch.stack(dist_worker.model()(img1, img2, iters=iters))
+    for r in range(world):
+        got = res[r][0]
+        assert got.shape == ref.shape
+        assert (got - ref).abs().max() < 5e-5, (r, (got - ref).abs().max())
+        assert (got - ref).abs().mean() < 1e-6
+    from raft_stereo_amd.shard import RowShardedStereo
+    hz = RowShardedStereo(dist_worker.model(), 0, 1).perconv_halos()
+    glob = RowShardedStereo._heights(H, 2, 3)
+    owns = [RowShardedStereo(dist_worker.model(), k, world)._own_rows(glob, hz) for k in range(world)]
+    assert owns[0][0] == 0 and owns[-1][1] == glob[0]
+    # the geometry the docstring describes: 1/16-res bands of 15-16 rows at
+    # world 8 (31-32 at world 4), i.e. about three net halos (5 rows) tall
+    band16 = sorted((b - a) >> 2 for a, b in owns)
+    assert band16[0] >= max(hz["net"]) and band16[-1] <= 496 // (4 * world) + 1, band16
+
+
 def test_gloo_perconv_overlap_equals_blocking():
     """Per-conv mode: exchanges posted at the update and waited for at the
     first reader give the same flows, bit for bit, as waiting right away."""
