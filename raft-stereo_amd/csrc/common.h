@@ -210,6 +210,7 @@ struct BuildBwdArgs {
 // Host-side launchers (defined in the .hip files, called by capi.cpp).
 hipError_t rc_launch_build_f32(const rc::BuildArgs &a, hipStream_t s);
 hipError_t rc_launch_build_split(rc::BuildArgs &a, hipStream_t s);     // may lower a.nfused
+hipError_t rc_launch_build_planes(rc::BuildArgs &a, hipStream_t s);   // dev library only
 hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s);   // may lower a.nfused
 hipError_t rc_launch_pool(const void *in, long long ld_in, void *out, long long ld_out, long rows,
                           int W_in, int bf16, hipStream_t s);

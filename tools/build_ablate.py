@@ -54,7 +54,8 @@ def main():
     with torch.no_grad():
         f1, f2, _ = bench.make_inputs(cfg, dev, seed=1)
 
-        knobs = {m.split("=")[0] for m in variants if isinstance(m, str) and "=" in m}
+        knobs = {kv.split("=")[0] for m in variants if isinstance(m, str) and "=" in m
+                 for kv in m.split("+")}
 
         def run(v):
             for k in knobs:
@@ -62,10 +63,11 @@ def main():
             if v == "exact":
                 os.environ["RAFTCORR_SPLIT_MODE"] = "0"
                 return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll, exact_f32=True)
-            if isinstance(v, str):   # NAME=VALUE: a dev knob over the product mode
+            if isinstance(v, str):   # NAME=VALUE[+NAME=VALUE]: dev knobs over the product mode
                 os.environ["RAFTCORR_SPLIT_MODE"] = "0"
-                k, val = v.split("=")
-                os.environ[k] = val
+                for kv in v.split("+"):
+                    k, val = kv.split("=")
+                    os.environ[k] = val
             else:
                 os.environ["RAFTCORR_SPLIT_MODE"] = str(v)
             return lambda: CorrBlock1D(f1, f2, num_levels=L, radius=r, low_latency=ll)
@@ -77,7 +79,8 @@ def main():
         # variants with math and stores (no 1/2/4 ablation bits) must
         # reproduce the product bit for bit
         for v in variants:
-            if ((isinstance(v, int) and v and not (v & 7)) or isinstance(v, str) and "=" in v) and ref is not None:
+            if ((isinstance(v, int) and v and not (v & 7)) or isinstance(v, str) and "=" in v
+                    and "MODE=" not in v) and ref is not None:
                 got = run(v)().corr_pyramid[:4]
                 res.setdefault("bit_identical", {})[str(v)] = all(
                     bool(torch.equal(x, y)) for x, y in zip(got, ref))
