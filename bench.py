@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 import pkgload  # noqa: E402
 
 pkgload.load()
-from raft_stereo_amd import CorrBlock1D, coords_grid  # noqa: E402
+from raft_stereo_amd import CorrBlock1D, _lib, coords_grid  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_ACHIEVABLE_GBS = 6290.0    # the same guide's measured float4 copy (report both)
@@ -601,9 +601,10 @@ def main():
     ap.add_argument("--shadow", default="default",
                     help="pyramid levels with an RC_SHADOW copy: 'default' (per-shape rule, "
                          "corr.default_shadow_levels), 'none', or a comma list such as 0,2")
-    ap.add_argument("--layout", default="rows", choices=("rows", "disparity"),
-                    help="CorrBlock1D pyramid layout: the reference's rows (default) or the opt-in "
-                         "disparity-major levels (RC_LAYOUT_DISPARITY, DESIGN.md §3.2h)")
+    ap.add_argument("--layout", default="rows", choices=("rows", "disparity", "records"),
+                    help="CorrBlock1D pyramid layout: the reference's rows (default), the opt-in "
+                         "disparity-major levels (RC_LAYOUT_DISPARITY, DESIGN.md §3.2h) or the bf16 "
+                         "record layout (RC_LAYOUT_RECORDS, §3.2i)")
     ap.add_argument("--field", default="random", choices=FIELDS,
                     help="coords field: random (SURVEY §8d, the headline), smooth or slant (coherent)")
     ap.add_argument("--network", action="store_true",
@@ -850,6 +851,7 @@ def main():
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     pair = blk._chain and (L == 2 or (L == 4 and 2 in written))
     lfamily = ("rc::lookup_sheared_pair_kernel" if args.layout == "disparity"
+               else "rc::lookup_records_kernel" if args.layout == "records"
                else "rc::lookup_pair_kernel" if pair else "rc::lookup_chain_kernel" if blk._chain
                else "rc::lookup_levelpar_kernel" if P < 65536 and L <= 4 else "rc::lookup_kernel")
     lname, lpmc = pmc_entry(pmc, lfamily)
@@ -911,6 +913,11 @@ def main():
                   f"levels {written} as S[b,h][k][w1], k = (w1 >> l) - j + W_l - 1 (the same values and "
                   "bytes as the rows), the lookup reads them with the disparity-major pair kernel; "
                   "corr_pyramid is gathered into rows only when read" if args.layout == "disparity" else
+                  f"record block (layout='records', RC_LAYOUT_RECORDS): the build writes levels {written} "
+                  f"as {_lib.rec_count(W2)} 128-B records per pixel row (the rows' values, 1.8x the "
+                  "shadowed rows' bytes; the extra writes are in the build's time, not in its "
+                  "algorithmic bytes), each lookup reads one line per pixel; corr_pyramid is "
+                  "gathered into rows only when read" if args.layout == "records" else
                   f"pool-chain block: the build writes pyramid levels {written} (levels "
                   f"{sorted(blk._shadow)} also as a half-line-shifted RC_SHADOW copy: those "
                   "writes are in the build's time, not in its algorithmic bytes); every lookup "

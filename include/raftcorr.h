@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RC_ABI_VERSION 9
+#define RC_ABI_VERSION 10
 
 /* element types */
 #define RC_F32  0
@@ -100,6 +100,31 @@ extern "C" {
  * under 4 GiB; RC_EUNSUPPORTED otherwise.  The other entry points refuse it. */
 #define RC_LAYOUT_DISPARITY 0x80000
 #define RC_SHEAR_ROWS(W2, W1, l) (((W2) >> (l)) + (((W1) - 1) >> (l)))
+
+/* Flag OR-ed into the pyr_dtype of rc_corr_build, rc_corr_lookup_chain and
+ * rc_corr_lookup_step (ABI v10): the 4-level bf16 pair layout's stored levels
+ * 0 and 2 as RECORDS -- one 128-byte line per pixel per lookup instead of two
+ * (DESIGN.md §3.2i).  pyr[0] is the record buffer: B*H*W1 pixel rows of
+ * RC_REC_COUNT(W2) records of RC_REC_SLOTS bf16 (RC_REC_BYTES each, pixel
+ * row p at pyr[0] + p * RC_REC_COUNT(W2) * RC_REC_BYTES, 16-byte aligned),
+ * record r holding
+ *     slots  0..25   level-2 elements 4r - 14 .. 4r + 11,
+ *     slots 26..63   level-0 elements 16r - 26 .. 16r + 11
+ * (zeros outside the level's width), so a pixel whose floor(x/2) lies in
+ * [8r - 8, 8r) reads every tap of all four levels (radius <= 4) from record
+ * r.  The values are the row layout's bit for bit, and so are the lookups.
+ * rc_corr_build: bf16 fmaps and pyramid, nbuf 3 with pyr[1] == pyr[2] ==
+ * NULL (pyr_ld ignored), 64 < W2 <= 320, D > 224, no shadow copies;
+ * rc_corr_lookup_chain / _step (chain != 0): RC_BF16, levels 4, radius 1..4,
+ * pyr[0] the records and pyr[1..3] NULL, widths[0] = W2; channels-last output
+ * allowed.  RC_EUNSUPPORTED otherwise; the other entry points refuse it.
+ * A pixel row's records take RC_REC_COUNT(W2) * 128 bytes, against about
+ * 2 * 2 * (W2 + W2 / 4) for the shadowed rows (2816 vs 1556 at W2 = 311):
+ * the build writes more, and each lookup reads half the lines. */
+#define RC_LAYOUT_RECORDS 0x100000
+#define RC_REC_SLOTS 64
+#define RC_REC_BYTES 128
+#define RC_REC_COUNT(W2) (((((W2) >> 1) + 15) >> 3) + 1)
 
 /* return codes */
 #define RC_OK            0

@@ -17,12 +17,19 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "raftcorr.h")
 RC_F32, RC_BF16 = 0, 1
 RC_OK, RC_EINVAL, RC_EUNSUPPORTED, RC_EHIP = 0, 1, 2, 3
 RC_MAX_LEVELS = 8
-ABI_VERSION = 9
+ABI_VERSION = 10
 RC_SHADOW = 0xFF00  # pyr_dtype flags: every stored level carries a line-phase shadow copy
 RC_OUT_CHANNELS_LAST = 0x10000   # pyr_dtype flag: NHWC lookup output (pair kernel)
 RC_BUILD_EXACT_F32 = 0x20000     # rc_corr_build flag: exact fp32 MFMA kernel instead of the split-bf16 one
 RC_GRAD_OVERWRITE = 0x40000      # rc_corr_lookup_backward_calls flag: write the sum, do not add
 RC_LAYOUT_DISPARITY = 0x80000    # rc_corr_build / rc_corr_lookup_chain: disparity-major levels 0, 2 (ABI v9)
+RC_LAYOUT_RECORDS = 0x100000     # rc_corr_build / _lookup_chain / _lookup_step: bf16 levels 0, 2 as records (ABI v10)
+RC_REC_SLOTS, RC_REC_BYTES = 64, 128
+
+
+def rec_count(W2):
+    """RC_REC_COUNT: 128-B records per pixel row of the record layout."""
+    return (((W2 >> 1) + 15) >> 3) + 1
 
 
 def shear_rows(W2, W1, l):

@@ -439,6 +439,114 @@ def lookup_sheared(sheared, coords, num_levels, radius, W2):
     return out
 
 
+# ------------------------------------------------------------ record layout
+# RC_LAYOUT_RECORDS (ABI v10): the 4-level bf16 pair layout's
+# stored levels 0 and 2 as rec_count(W2) 128-B records per pixel row; record r
+# holds level-2 elements 4r-14 .. 4r+11 (slots 0..25) and level-0 elements
+# 16r-26 .. 16r+11 (slots 26..63), so a pixel's lookup reads one line.
+
+_REC_L2_SLOTS = 26
+
+
+def records_supported(fmap1, fmap2, num_levels, radius, pyramid_dtype):
+    """Why CorrBlock1D(layout="records") cannot serve these inputs, or None."""
+    if pyramid_dtype != torch.bfloat16:
+        return "a bf16 pyramid only (bf16 fmaps, or pyramid_dtype=torch.bfloat16)"
+    if num_levels != 4 or not 1 <= radius <= 4:
+        return "4 levels, radius 1..4"
+    B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+    if not 64 < W2 <= 320:
+        return "64 < W2 <= 320 (one workgroup tile spans the row)"
+    if D <= 224:
+        return "D > 224 (at least 8 K stages per tile)"
+    if D * H * max(W1, W2) * 2 >= 1 << 30:
+        return "fmap images under 1 GiB"
+    return None
+
+
+def build_records(fmap1, fmap2):
+    """rc_corr_build with RC_LAYOUT_RECORDS: a (B*H*W1, rec_count(W2), 64)
+    bf16 tensor.  fp32/fp16 fmaps are rounded to bf16 first (round to nearest
+    even, as the bf16 kernels do on load)."""
+    B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+    f1 = fmap1.to(torch.bfloat16).contiguous()
+    f2 = fmap2.to(torch.bfloat16).contiguous()
+    NR = _lib.rec_count(W2)
+    rec = torch.empty((B * H * W1, NR, _lib.RC_REC_SLOTS), dtype=torch.bfloat16, device=f1.device)
+    if B * H * W1 == 0:
+        return rec
+    with torch.cuda.device(f1.device):
+        rc = _lib.lib().rc_corr_build(
+            f1.data_ptr(), f2.data_ptr(), _lib.RC_BF16, B, D, H, W1, W2,
+            _lib.ptr_array([rec.data_ptr(), None, None]), _lib.long_array([W2, W2 >> 1, W2 >> 2]), 3,
+            _lib.RC_BF16 | _lib.RC_LAYOUT_RECORDS, _stream(f1.device))
+    _lib.check(rc, "rc_corr_build")
+    return rec
+
+
+def records_level(rec, l, W2):
+    """Level l (0 or 2) of a record-layout pyramid as the reference's
+    (B*H*W1, 1, 1, W2 >> l) rows (row-padded buffer): the same values,
+    gathered from the records that hold them."""
+    P, NR, S = rec.shape
+    W = W2 >> l
+    e = torch.arange(W, device=rec.device)
+    if l == 0:
+        r = ((e + 26) >> 4).clamp(max=NR - 1)
+        slot = _REC_L2_SLOTS + e - (16 * r - 26)
+    elif l == 2:
+        r = ((e + 14) >> 2).clamp(max=NR - 1)
+        slot = e - (4 * r - 14)
+    else:
+        raise ValueError("records hold levels 0 and 2")
+    out = _level_buffer(P, W, torch.bfloat16, rec.device, True)
+    if P:
+        out.copy_(rec.view(P, NR * S)[:, r * S + slot].view(P, 1, 1, W))
+    return out
+
+
+def _records_args(rec, W2):
+    ptrs = _lib.ptr_array([rec.data_ptr(), None, None, None])
+    widths = _lib.int_array([W2 >> l for l in range(4)])
+    lds = _lib.long_array([W2 >> l for l in range(4)])
+    return ptrs, widths, lds
+
+
+def _check_records_coords(rec, coords):
+    _require_hip(coords, "coords")
+    if coords.dim() != 4 or coords.shape[1] < 1:
+        raise RuntimeError("CorrBlock1D: coords must be (B, 2, H, W1)")
+    if coords.dtype != torch.float32:
+        raise RuntimeError(f"CorrBlock1D: coords dtype {coords.dtype} != float32 (model.py:275)")
+    B, _, H, W1 = coords.shape
+    if B * H * W1 != rec.shape[0]:
+        raise RuntimeError(f"CorrBlock1D: coords {tuple(coords.shape)} do not match the volume's "
+                           f"{rec.shape[0]} rows (view at model.py:312)")
+    if coords.device != rec.device:
+        raise RuntimeError("CorrBlock1D: coords and pyramid on different devices")
+
+
+def lookup_records(rec, coords, radius, W2, channels_last=False):
+    """rc_corr_lookup_chain with RC_LAYOUT_RECORDS: the pair kernel's
+    results (bit for bit) from the records, one 128-B line per pixel."""
+    _check_records_coords(rec, coords)
+    B, _, H, W1 = coords.shape
+    x = coords[:, 0]
+    if x.stride(2) != 1 or x.stride(1) != W1:
+        x = x.contiguous()
+    cbs = x.stride(0) if B > 1 else H * W1
+    out = _lookup_out(B, 4 * (2 * radius + 1), H, W1, coords.device, channels_last)
+    if B * H * W1 == 0:
+        return out
+    ptrs, widths, lds = _records_args(rec, W2)
+    dt = _lib.RC_BF16 | _lib.RC_LAYOUT_RECORDS | (_lib.RC_OUT_CHANNELS_LAST if channels_last else 0)
+    with torch.cuda.device(coords.device):
+        rc = _lib.lib().rc_corr_lookup_chain(ptrs, widths, lds, dt, 4, radius, x.data_ptr(), cbs, B, H, W1,
+                                             out.data_ptr(), _stream(coords.device))
+    _lib.check(rc, "rc_corr_lookup_chain")
+    return out
+
+
 # ----------------------------------------------------------------- backward
 
 class _GradLevels(list):
@@ -763,12 +871,21 @@ class CorrBlock1D:
         # lookups bit for bit, faster on the network's coherent coordinates,
         # slower on independent random ones.  corr_pyramid is gathered into
         # the reference's rows when read.
-        if layout not in ("rows", "disparity"):
-            raise ValueError(f"CorrBlock1D: layout={layout!r}: 'rows' or 'disparity'")
+        # layout="records" (opt-in, RC_LAYOUT_RECORDS): the
+        # bf16 pair layout's levels 0 and 2 as 128-B records, one line per
+        # pixel per lookup instead of two; the same values and lookups bit for
+        # bit; the build writes 1.8x the bytes of the shadowed rows.
+        if layout not in ("rows", "disparity", "records"):
+            raise ValueError(f"CorrBlock1D: layout={layout!r}: 'rows', 'disparity' or 'records'")
         self.layout = layout
         self._sheared = None
+        self._records = None
         if layout == "disparity":
             self._init_sheared(fmap1, fmap2, num_levels, radius, pyramid_dtype, lazy_levels, shadow,
+                               channels_last, low_latency, grad_shadow, exact_f32, grad_deferred)
+            return
+        if layout == "records":
+            self._init_records(fmap1, fmap2, num_levels, radius, pyramid_dtype, lazy_levels, shadow,
                                channels_last, low_latency, grad_shadow, exact_f32, grad_deferred)
             return
         # lookup outputs in NHWC memory order (torch.channels_last): same
@@ -878,13 +995,44 @@ class CorrBlock1D:
                                      num_levels, radius, None, deferred=grad_deferred)
             self._token = _BuildFn.apply(fmap1, fmap2, self._state)
 
+    def _init_records(self, fmap1, fmap2, num_levels, radius, pyramid_dtype, lazy_levels, shadow,
+                      channels_last, low_latency, grad_shadow, exact_f32, grad_deferred):
+        if pyramid_dtype is None:
+            pyramid_dtype = torch.bfloat16
+        why = records_supported(fmap1, fmap2, num_levels, radius, pyramid_dtype)
+        if why is None and (low_latency or shadow or grad_shadow or exact_f32 or lazy_levels is False):
+            why = ("no low_latency, shadow, grad_shadow, exact_f32 or eager levels (the records replace "
+                   "the stored rows and their shadow copies)")
+        if why is not None:
+            raise ValueError(f"CorrBlock1D(layout='records'): {why}")
+        self.pyramid_dtype = pyramid_dtype
+        self.channels_last = bool(channels_last)
+        B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+        self._shape = (B, H, W1, W2)
+        self._chain, self._shadow = True, frozenset()
+        grad = torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad)
+        with torch.no_grad():
+            self._records = build_records(fmap1, fmap2)
+        self._levels = [None] * (num_levels + 1)
+        self._state = self._token = None
+        if grad:
+            self._state = _GradState(B * H * W1, [W2 >> i for i in range(num_levels)], fmap1.device,
+                                     num_levels, radius, None, deferred=grad_deferred)
+            self._token = _BuildFn.apply(fmap1, fmap2, self._state)
+
     @property
     def corr_pyramid(self):
         """num_levels+1 tensors (B*H*W1, 1, 1, W2 >> l) as model.py:287-295;
-        lazily pooled levels are built on first access (layout="disparity":
-        the stored levels gathered into rows, the others pooled from them)."""
+        lazily pooled levels are built on first access (layout="disparity" /
+        "records": the stored levels gathered into rows, the others pooled
+        from them)."""
         if any(t is None for t in self._levels):
             with torch.no_grad():
+                if self._records is not None:
+                    W2 = self._shape[3]
+                    for l in (0, 2):
+                        if self._levels[l] is None:
+                            self._levels[l] = records_level(self._records, l, W2)
                 if self._sheared is not None:
                     B, H, W1, W2 = self._shape
                     for l, S in self._sheared.items():
@@ -899,7 +1047,7 @@ class CorrBlock1D:
     def levels_stored(self):
         """Indices of the pyramid levels currently held in memory (either
         layout)."""
-        held = set(self._sheared or ())
+        held = set(self._sheared or ()) | ({0, 2} if self._records is not None else set())
         return sorted(held | {l for l, t in enumerate(self._levels) if t is not None})
 
     @corr_pyramid.setter
@@ -909,6 +1057,7 @@ class CorrBlock1D:
         self._chain = False
         self._shadow = frozenset()
         self._sheared = None
+        self._records = None
         self.layout = "rows"
 
     def _read_levels(self):
@@ -920,6 +1069,8 @@ class CorrBlock1D:
         return self.corr_pyramid[:L]
 
     def _lookup(self, coords):
+        if self._records is not None:
+            return lookup_records(self._records, coords, self.radius, self._shape[3], self.channels_last)
         if self._sheared is not None:
             return lookup_sheared(self._sheared, coords, self.num_levels, self.radius, self._shape[3])
         if self._chain:
@@ -945,7 +1096,10 @@ class CorrBlock1D:
             raise RuntimeError("CorrBlock1D.lookup_step is inference-only")
         if self._sheared is not None:
             raise RuntimeError("CorrBlock1D.lookup_step: not available with layout='disparity'")
-        _check_coords(self._levels, coords1)
+        if self._records is not None:
+            _check_records_coords(self._records, coords1)
+        else:
+            _check_coords(self._levels, coords1)
         B, C2, H, W1 = coords1.shape
         if C2 != 2:
             raise RuntimeError("lookup_step: coords1 must be (B, 2, H, W1)")
@@ -967,11 +1121,15 @@ class CorrBlock1D:
             raise RuntimeError("lookup_step: out must be a contiguous fp32 (B, 2, H, W1) tensor")
         flow = torch.empty_like(c1)
         L, r = self.num_levels, self.radius
-        cl = self.channels_last and self._chain and _pair_layout(self._levels, L)
+        cl = self.channels_last and self._chain and (self._records is not None or _pair_layout(self._levels, L))
         corr = _lookup_out(B, L * (2 * r + 1), H, W1, c1.device, cl)
         if B * H * W1 == 0:
             return corr, new, flow
-        if self._chain:
+        if self._records is not None:
+            keep = self._records
+            ptrs, widths, lds = _records_args(self._records, self._shape[3])
+            dt = _lib.RC_BF16 | _lib.RC_LAYOUT_RECORDS
+        elif self._chain:
             keep, ptrs, widths, lds, dt = _chain_args(self._levels, L, self._shadow)
         else:
             keep, ptrs, widths, lds, dt = _level_args(self._read_levels(), L)
@@ -995,8 +1153,8 @@ class CorrBlock1D:
         if torch.is_grad_enabled() and (self._token is not None or weight.requires_grad):
             raise RuntimeError("CorrBlock1D.lookup_convc1 is inference-only; use "
                                "convc1(block(coords)) when gradients are needed")
-        if self._sheared is not None:
-            raise RuntimeError("CorrBlock1D.lookup_convc1: not available with layout='disparity'")
+        if self._sheared is not None or self._records is not None:
+            raise RuntimeError(f"CorrBlock1D.lookup_convc1: not available with layout={self.layout!r}")
         return lookup_convc1(self._read_levels(), coords, self.num_levels, self.radius, weight,
                              bias, relu)
 

@@ -37,16 +37,23 @@ long long shadow_offset(long long rows, long long ld, int esize) { return RC_SHA
 
 // pyr_dtype bits an entry point accepts: the element type (low byte), the
 // RC_SHADOW_LEVEL bits and, where the pair kernel serves it, RC_OUT_CHANNELS_LAST.
-int check_flags(const char *who, int pyr_dtype, bool allow_cl, bool build = false, bool allow_disp = false) {
+int check_flags(const char *who, int pyr_dtype, bool allow_cl, bool build = false, bool allow_disp = false,
+                bool allow_rec = false) {
     const unsigned known = 0xFFu | RC_SHADOW | (allow_cl ? (unsigned)RC_OUT_CHANNELS_LAST : 0u) |
                            (build ? (unsigned)RC_BUILD_EXACT_F32 : 0u) |
-                           (allow_disp ? (unsigned)RC_LAYOUT_DISPARITY : 0u);
+                           (allow_disp ? (unsigned)RC_LAYOUT_DISPARITY : 0u) |
+                           (allow_rec ? (unsigned)RC_LAYOUT_RECORDS : 0u);
     if (!allow_cl && (pyr_dtype & RC_OUT_CHANNELS_LAST))
         return fail(RC_EUNSUPPORTED, "%s: RC_OUT_CHANNELS_LAST is only defined for "
                     "rc_corr_lookup_chain / rc_corr_lookup_step", who);
     if (!allow_disp && (pyr_dtype & RC_LAYOUT_DISPARITY))
         return fail(RC_EUNSUPPORTED, "%s: RC_LAYOUT_DISPARITY is only defined for "
                     "rc_corr_build / rc_corr_lookup_chain", who);
+    if (!allow_rec && (pyr_dtype & RC_LAYOUT_RECORDS))
+        return fail(RC_EUNSUPPORTED, "%s: RC_LAYOUT_RECORDS is only defined for "
+                    "rc_corr_build / rc_corr_lookup_chain / rc_corr_lookup_step", who);
+    if ((pyr_dtype & RC_LAYOUT_DISPARITY) && (pyr_dtype & RC_LAYOUT_RECORDS))
+        return fail(RC_EINVAL, "%s: RC_LAYOUT_DISPARITY and RC_LAYOUT_RECORDS exclude each other", who);
     if ((unsigned)pyr_dtype & ~known)
         return fail(RC_EINVAL, "%s: unknown pyr_dtype flag bits 0x%x", who, (unsigned)pyr_dtype & ~known);
     return RC_OK;
@@ -67,9 +74,10 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
                              int H, int W1, int W2, void *const *pyr, const long *pyr_ld, int nbuf,
                              int pyr_dtype, void *stream) {
     g_err[0] = 0;
-    if (int e = check_flags("rc_corr_build", pyr_dtype, false, true, true)) return e;
+    if (int e = check_flags("rc_corr_build", pyr_dtype, false, true, true, true)) return e;
     const bool exact_f32 = (pyr_dtype & RC_BUILD_EXACT_F32) != 0;
     const bool disp = (pyr_dtype & RC_LAYOUT_DISPARITY) != 0;
+    const bool rec = (pyr_dtype & RC_LAYOUT_RECORDS) != 0;
     const unsigned shmask = ((unsigned)pyr_dtype >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits
     pyr_dtype &= 0xFF;
     if (B < 0 || D <= 0 || H < 0 || W1 < 0 || W2 <= 0)
@@ -105,6 +113,19 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
                 return fail(RC_EUNSUPPORTED, "rc_corr_build: disparity-major level %d exceeds 4 GiB", l);
         }
     }
+    if (rec) {   // RC_LAYOUT_RECORDS: the bf16 ring build's deferred epilogue, one tile per row
+        if (fmap_dtype != RC_BF16 || pyr_dtype != RC_BF16 || exact_f32 || shmask)
+            return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_RECORDS needs bf16 fmaps and pyramid "
+                        "and no shadow copies");
+        if (nbuf != 3 || pyr[1] || pyr[2])
+            return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_RECORDS stores the 4-level pair layout: "
+                        "nbuf 3 with pyr[0] the records and pyr[1], pyr[2] NULL");
+        if (W2 <= 64 || W2 > 320 || D <= 224)
+            return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_RECORDS needs 64 < W2 <= 320 and D > 224 "
+                        "(W2=%d D=%d)", W2, D);
+        if ((long long)D * H * (W1 > W2 ? W1 : W2) * 2 >= (1LL << 30))
+            return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_RECORDS: fmap image over 1 GiB");
+    }
     if ((long long)B * H * W1 == 0) return RC_OK;
     if (!fmap1 || !fmap2 || !aligned16(fmap1) || !aligned16(fmap2))
         return fail(RC_EINVAL, "rc_corr_build: feature maps must be non-null and 16-byte aligned");
@@ -116,7 +137,7 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
         if (!pyr[l] && may_skip) continue;
         if (!pyr[l] || !aligned16(pyr[l]))
             return fail(RC_EINVAL, "rc_corr_build: pyramid buffer %d null or not 16-byte aligned", l);
-        if (!disp && pyr_ld && pyr_ld[l] < (long)(W2 >> l))
+        if (!disp && !rec && pyr_ld && pyr_ld[l] < (long)(W2 >> l))
             return fail(RC_EINVAL, "rc_corr_build: row stride %ld of level %d < width %d", pyr_ld[l],
                         l, W2 >> l);
     }
@@ -126,7 +147,11 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     a.f2 = fmap2;
     a.B = B; a.D = D; a.H = H; a.W1 = W1; a.W2 = W2;
     a.nfused = nfused;
-    for (int l = 0; l < a.nfused; ++l) {
+    if (rec) {
+        a.rec = pyr[0];
+        a.rec_nr = RC_REC_COUNT(W2);
+    }
+    for (int l = 0; l < a.nfused && !rec; ++l) {
         a.lvl[l] = pyr[l];
         a.ld[l] = pyr_ld ? pyr_ld[l] : (W2 >> l);
         if ((shmask >> l & 1u) && pyr[l])
@@ -154,6 +179,8 @@ extern "C" int rc_corr_build(const void *fmap1, const void *fmap2, int fmap_dtyp
     else if (!exact_f32) e = rc_launch_build_split(a, s);
     if (e == hipErrorNotSupported && disp)
         return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_DISPARITY: shape outside the split build");
+    if (e == hipErrorNotSupported && rec)
+        return fail(RC_EUNSUPPORTED, "rc_corr_build: RC_LAYOUT_RECORDS: shape outside the records build");
     if (e == hipErrorNotSupported && !bf16_mma) e = rc_launch_build_f32(a, s);
     int rc = hip_rc(e, "rc_corr_build: volume launch");
     if (rc) return rc;
@@ -199,6 +226,7 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
                 bool *empty, bool allow_null = false) {
     *empty = false;
     const bool disp = (pyr_dtype & RC_LAYOUT_DISPARITY) != 0;     // rows of W1 (or more) per diagonal
+    const bool rec = (pyr_dtype & RC_LAYOUT_RECORDS) != 0;        // pyr[0] = the records
     const unsigned shmask = ((unsigned)pyr_dtype >> 8) & 0xFFu;   // RC_SHADOW_LEVEL bits
     pyr_dtype &= 0xFF;
     if (levels < 1 || levels > RC_MAX_LEVELS)
@@ -231,6 +259,12 @@ int prep_lookup(const char *who, const void *const *pyr, const int *widths, cons
         a.lvl[i] = pyr[i];
         a.W[i] = widths[i];
         a.ld[i] = pyr_ld ? pyr_ld[i] : widths[i];
+        if (rec) {
+            if (i > 0) return fail(RC_EINVAL, "%s: RC_LAYOUT_RECORDS: pyr[%d] must be NULL", who, i);
+            a.ld[0] = widths[0];
+            a.rec_nr = RC_REC_COUNT(widths[0]);
+            continue;
+        }
         if (disp) {
             if (a.ld[i] < W1 || a.ld[i] % 4)
                 return fail(RC_EINVAL, "%s: disparity-major row stride %lld of level %d must be >= W1 = %d "
@@ -267,14 +301,14 @@ namespace {
 // for 2 levels, or for 4 levels when level 2 is given; otherwise the level-1
 // chain kernel (reads levels 0 and 1) for 3-4 levels.
 int chain_kind(const char *who, const void *const *pyr, const int *widths, int levels, int radius,
-               bool *pair) {
+               bool *pair, bool rec = false) {
     if (levels < 2 || levels > 4 || radius < 1 || radius > 4)
         return fail(RC_EUNSUPPORTED, "%s: levels 2..4 and radius 1..4 only", who);
     for (int i = 1; i < levels; ++i)
         if (widths[i] != widths[i - 1] / 2)
             return fail(RC_EINVAL, "%s: width %d of level %d is not floor(%d/2)", who, widths[i], i,
                         widths[i - 1]);
-    *pair = levels == 2 || (levels == 4 && pyr[2] != nullptr);
+    *pair = levels == 2 || (levels == 4 && (pyr[2] != nullptr || rec));
     // the pair kernel's window argument holds for widths up to 2^16 (lookup.hip)
     if (*pair && widths[0] > 65536)
         return fail(RC_EUNSUPPORTED, "%s: level-0 width %d > 65536 for the pair kernel", who,
@@ -326,16 +360,20 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
-    if (int e = check_flags("rc_corr_lookup_chain", pyr_dtype, true, false, true)) return e;
+    if (int e = check_flags("rc_corr_lookup_chain", pyr_dtype, true, false, true, true)) return e;
     int rc = prep_lookup("rc_corr_lookup_chain", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords_x, coord_batch_stride, B, H, W1, out, a, &empty, true);
     if (rc) return rc;
     const bool cl = (pyr_dtype & RC_OUT_CHANNELS_LAST) != 0;
     const bool disp = (pyr_dtype & RC_LAYOUT_DISPARITY) != 0;
+    const bool rec = (pyr_dtype & RC_LAYOUT_RECORDS) != 0;
     const bool shadowed = ((unsigned)pyr_dtype & RC_SHADOW) != 0;
     pyr_dtype &= 0xFF;
     bool pair;
-    if ((rc = chain_kind("rc_corr_lookup_chain", pyr, widths, levels, radius, &pair))) return rc;
+    if ((rc = chain_kind("rc_corr_lookup_chain", pyr, widths, levels, radius, &pair, rec))) return rc;
+    if (rec && (levels != 4 || pyr_dtype != RC_BF16 || shadowed))
+        return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: RC_LAYOUT_RECORDS needs the 4-level bf16 pair "
+                    "layout and no shadow copies");
     if (disp && (!pair || pyr_dtype != RC_F32 || cl || shadowed))
         return fail(RC_EUNSUPPORTED, "rc_corr_lookup_chain: RC_LAYOUT_DISPARITY needs the fp32 pair layout "
                     "(2 levels, or 4 with level 2 given), NCHW output and no shadow copies");
@@ -347,7 +385,7 @@ extern "C" int rc_corr_lookup_chain(const void *const *pyr, const int *widths, c
     if (empty) return RC_OK;
     a.out = out;
     a.out_cl = cl;
-    if ((rc = chain_strides("rc_corr_lookup_chain", a, pair, pyr_dtype == RC_BF16))) return rc;
+    if (!rec && (rc = chain_strides("rc_corr_lookup_chain", a, pair, pyr_dtype == RC_BF16))) return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     return hip_rc(pair ? rc_launch_lookup_pair(a, radius, pyr_dtype == RC_BF16, s)
                        : rc_launch_lookup_chain(a, radius, s),
@@ -362,7 +400,10 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
     g_err[0] = 0;
     rc::LookupArgs a;
     bool empty;
-    if (int e = check_flags("rc_corr_lookup_step", pyr_dtype, true)) return e;
+    if (int e = check_flags("rc_corr_lookup_step", pyr_dtype, true, false, false, true)) return e;
+    const bool rec = (pyr_dtype & RC_LAYOUT_RECORDS) != 0;
+    const bool shadowed = ((unsigned)pyr_dtype & RC_SHADOW) != 0;
+    if (rec && !chain) return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: RC_LAYOUT_RECORDS needs chain != 0");
     int rc = prep_lookup("rc_corr_lookup_step", pyr, widths, pyr_ld, pyr_dtype, levels, radius,
                          coords1, 2L * H * W1, B, H, W1, out, a, &empty, chain != 0);
     if (rc || empty) return rc;
@@ -372,10 +413,13 @@ extern "C" int rc_corr_lookup_step(const void *const *pyr, const int *widths, co
         return fail(RC_EINVAL, "rc_corr_lookup_step: null coords1_out / flow_out");
     bool pair = false;
     if (chain) {
-        if ((rc = chain_kind("rc_corr_lookup_step", pyr, widths, levels, radius, &pair))) return rc;
+        if ((rc = chain_kind("rc_corr_lookup_step", pyr, widths, levels, radius, &pair, rec))) return rc;
         if (pyr_dtype != RC_F32 && !pair)
             return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: a bf16 pyramid needs the pair layout");
-        if ((rc = chain_strides("rc_corr_lookup_step", a, pair, pyr_dtype == RC_BF16))) return rc;
+        if (rec && (levels != 4 || pyr_dtype != RC_BF16 || shadowed))
+            return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: RC_LAYOUT_RECORDS needs the 4-level bf16 pair "
+                        "layout and no shadow copies");
+        if (!rec && (rc = chain_strides("rc_corr_lookup_step", a, pair, pyr_dtype == RC_BF16))) return rc;
     }
     if (cl && !pair)
         return fail(RC_EUNSUPPORTED, "rc_corr_lookup_step: RC_OUT_CHANNELS_LAST needs the pair layout");

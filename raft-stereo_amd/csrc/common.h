@@ -123,7 +123,21 @@ struct BuildArgs {
     // RC_LAYOUT_DISPARITY (ABI v9): levels 0 and 2 disparity-major, shk[l]
     // rows (diagonals) of ld[l] elements per row block; 0 = row layout
     long long shk[kMaxLevels];
+    // RC_LAYOUT_RECORDS (ABI v10): levels 0 and 2 as rec_nr 128-B records
+    // per pixel row at rec (the bf16 ring build's deferred epilogue)
+    void *rec;
+    int rec_nr;
 };
+
+// RC_LAYOUT_RECORDS geometry (include/raftcorr.h): record r of a pixel row
+// holds level-2 elements 4r - 14 .. 4r + 11 in slots 0..25 and level-0
+// elements 16r - 26 .. 16r + 11 in slots 26..63 (bf16), so a pixel whose
+// level-1 centre floor(x/2) lies in [8r - 8, 8r) finds the spans of all four
+// levels (radius <= 4) in that one line.
+constexpr int kRecSlots = 64, kRecL2Slots = 26;
+constexpr int kRecM0 = -8;                       // level-1 centre of record 0's first pixel
+__host__ __device__ constexpr int rec_e0(int r) { return 16 * r + 2 * kRecM0 - 10; }   // first level-0 element
+__host__ __device__ constexpr int rec_e2(int r) { return 4 * r + kRecM0 / 2 - 10; }    // first level-2 element
 
 struct LookupArgs {
     const void *lvl[kMaxLevels];
@@ -150,6 +164,8 @@ struct LookupArgs {
     // RC_LAYOUT_DISPARITY (ABI v9): levels 0 and 2 disparity-major, shk[l]
     // rows (diagonals) of ld[l] elements per row block; 0 = row layout
     long long shk[kMaxLevels];
+    // RC_LAYOUT_RECORDS (ABI v10): lvl[0] = the records, rec_nr per pixel row
+    int rec_nr;
 };
 
 // Backward of the lookup: level gradients (fp32, row stride ld[i] % 4 == 0).

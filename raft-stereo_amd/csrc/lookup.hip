@@ -880,6 +880,150 @@ __global__ __launch_bounds__(256) void lookup_sheared_pair_kernel(LookupArgs a) 
     }
 }
 
+// ---- lookup over the record layout (RC_LAYOUT_RECORDS, bf16, 4 levels) ----
+// Each pixel row holds a.rec_nr 128-B records (rc_corr_build with the flag;
+// geometry in common.h): record r has level-2 elements rec_e2(r) .. +25 in
+// slots 0..25 and level-0 elements rec_e0(r) .. +37 in slots 26..63, so a
+// pixel whose level-1 centre m1 = floor(x/2) lies in [8r - 8, 8r) finds both
+// of its pair spans (level 0's from 2(m1 - R - 1), level 2's from
+// 2(floor(m1/4) - R - 1)) in record r: ONE 128-B line per pixel instead of
+// two.  A pixel outside the records' m1 range takes the
+// nearest record; its exact spans are then empty or lie at the row edge that
+// record covers.  The chunks are read with issue_pair's exact-span predicate
+// and finish_pair runs unchanged, so the output is the row layout's bit for
+// bit.
+
+// issue_pair over a record: level-lo element e sits in slot e - e_first + slot_first
+template <int R>
+__device__ __forceinline__ void issue_record_pair(PairSpan<R, true> &ps, const LookupArgs &a, int lo, float x,
+                                                  const __amdgpu_buffer_rsrc_t &rs, uint32_t rbyte, int e_first,
+                                                  int slot_first) {
+    typedef PairSpan<R, true> PS;
+    const int Wlo = a.W[lo], Whi = a.W[lo + 1];
+    const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
+    ps.inwin = (xhi > -(float)(R + 4)) && (xhi < (float)(Whi + R + 4));
+    ps.m = ps.inwin ? floorf(xhi) : 0.0f;
+    ps.n = ps.inwin ? floorf(xlo) : 0.0f;
+    const int dd = (int)ps.n - 2 * (int)ps.m;
+    ps.valid = ps.inwin && (dd == 0 || dd == 1);
+    int lo_e = 0x7FFFFFFF, hi_e = -1;
+    if (ps.inwin) {
+        int f, l;
+        tap_span<R>(xlo, Wlo, f, l);
+        if (f <= l) { lo_e = f; hi_e = l; }
+        tap_span<R>(xhi, Whi, f, l);
+        if (f <= l) { lo_e = min(lo_e, 2 * f); hi_e = max(hi_e, 2 * l + 1); }
+    }
+    const int sslot = 2 * ((int)ps.m - R - 1) - e_first + slot_first;   // span start (even)
+    const int cb = sslot >= 0 ? sslot & ~7 : -((-sslot + 7) & ~7);      // chunk base (floor to 8)
+    ps.sh = sslot - cb;
+    const int slo = lo_e - e_first + slot_first, shi = hi_e - e_first + slot_first;
+#pragma unroll
+    for (int k = 0; k < PS::NC; ++k) {
+        const int cs = cb + 8 * k;
+        const bool ok = lo_e <= hi_e && cs <= shi && cs + 7 >= slo && cs >= 0 && cs + 8 <= kRecSlots;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (int)(rbyte + 2u * (uint32_t)cs) : (int)0xFFFFFF00u,
+                                                             0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ps.q[k][c] = v[c];
+    }
+}
+
+// finish_pair's memory path over the records (a subnormal x, the only way to
+// break n = 2m + dd): level lo (0 or 2) element e from a record that holds
+// it, level lo + 1 the bf16-rounded pairwise mean, the ops of level_taps_mem
+template <int R, class Sink>
+__device__ __forceinline__ void record_taps_mem(const LookupArgs &a, const uint16_t *rec, int lo, float x,
+                                                Sink &&sink) {
+    constexpr int T = 2 * R + 1;
+    const int NR = a.rec_nr;
+    auto elem = [&](long long e) {
+        int r = lo == 0 ? (int)((e - rec_e0(0)) >> 4) : (int)((e - rec_e2(0)) >> 2);
+        r = r < NR ? r : NR - 1;
+        const int slot = lo == 0 ? kRecL2Slots + (int)e - rec_e0(r) : (int)e - rec_e2(r);
+        return bf16_to_f32(rec[r * kRecSlots + slot]);
+    };
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const int W = a.W[lo + half];
+        const float Wm1 = (float)(W - 1), hw = Wm1 / 2.0f;
+        const DivRN dv = div_prep(Wm1);
+        const float xl = x / (float)(1 << (lo + half));
+        for (int t = 0; t < T; ++t) {
+            const float xt = (float)(t - R) + xl;
+            const float xn = div_rn(2.0f * xt, dv) - 1.0f;
+            const float xp = (xn + 1.0f) * hw;
+            const float x0 = floorf(xp);
+            const float wt1 = xp - x0, wt0 = 1.0f - wt1;
+            const bool ok0 = (x0 >= 0.0f) && (x0 <= Wm1);
+            const bool ok1 = (x0 + 1.0f >= 0.0f) && (x0 + 1.0f <= Wm1);
+            const long long e = (long long)x0;
+            float v0 = 0.0f, v1 = 0.0f;
+            if (half == 0) {
+                if (ok0) v0 = elem(e);
+                if (ok1) v1 = elem(e + 1);
+            } else {
+                if (ok0) v0 = round_bf16((elem(2 * e) + elem(2 * e + 1)) * 0.5f);
+                if (ok1) v1 = round_bf16((elem(2 * e + 2) + elem(2 * e + 3)) * 0.5f);
+            }
+            sink((lo + half) * T + t, fmaf(wt1, v1, wt0 * v0));
+        }
+    }
+}
+
+// CL: channels-last output (RC_OUT_CHANNELS_LAST) through the per-wave LDS
+// tile of lookup_pair_kernel; else NCHW dword stores.
+template <int R, bool CL>
+__global__ __launch_bounds__(256) void lookup_records_kernel(LookupArgs a) {
+    constexpr int NL = 4, C = NL * (2 * R + 1);
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const PairPixel q = pair_pixel<R, NL>(a, (long long)blk * 256);
+    const int NR = a.rec_nr;
+    // the pixel's record (clamped as floats before the integer cast: NaN -> 0)
+    float mf = floorf(q.x / 2.0f);
+    mf = fminf(fmaxf(mf, (float)kRecM0), (float)(kRecM0 + 8 * NR - 1));
+    const int r = ((int)mf - kRecM0) >> 3;
+    const uint16_t *blkrec = static_cast<const uint16_t *>(a.lvl[0]) + q.pblk * (long long)NR * kRecSlots;
+    // the block's records (< 4 GiB: 256 rows of <= 22 lines)
+    const auto rs = make_rsrc(blkrec, clamp_bytes((a.P - q.pblk) * (long long)NR * kRecSlots * 2));
+    const uint32_t rbyte = (uint32_t)((q.lrow * NR + r) * kRecSlots * 2);
+    PairSpan<R, true> sp[2];
+    issue_record_pair<R>(sp[0], a, 0, q.x, rs, rbyte, rec_e0(r), kRecL2Slots);
+    issue_record_pair<R>(sp[1], a, 2, q.x, rs, rbyte, rec_e2(r), 0);
+    __shared__ __attribute__((aligned(16))) float ctile[CL ? 4 * 64 * C : 1];
+    auto sink = [&](int ch, float v) {
+        if constexpr (CL) ctile[(threadIdx.x >> 6) * 64 * C + (threadIdx.x & 63) * C + ch] = v;
+        else if (q.active) q.outp[(long long)ch * a.HW] = v;
+    };
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (__builtin_expect(sp[k].inwin && !sp[k].valid, 0)) {
+            record_taps_mem<R>(a, blkrec + q.lrow * (long long)NR * kRecSlots, 2 * k, q.x, sink);
+            continue;
+        }
+        finish_pair<R, true, true>(sp[k], a, 2 * k, q.x, q.pp, sink);
+    }
+    if constexpr (CL) {
+        const int lane = threadIdx.x & 63;
+        const long long pw = q.pblk + (threadIdx.x & ~63);
+        const float *t = ctile + (threadIdx.x >> 6) * 64 * C;
+        const long long lim = (a.P - pw < 64 ? a.P - pw : 64) * C;
+#pragma unroll
+        for (int k = 0; k < (16 * C + 63) / 64; ++k) {
+            const int e = (k * 64 + lane) * 4;
+            if (e >= 64 * C || e >= lim) continue;
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(t + e);
+            if (e + 4 <= lim) {
+                *reinterpret_cast<f32x4 *>(a.out + pw * C + e) = v;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (e + j < lim) a.out[pw * C + e + j] = v[j];
+            }
+        }
+    }
+}
+
 template <int R, int NL, bool BF16, bool EXACT, int BS = 256, int WPE = 1>
 static void launch_k(const LookupArgs &a, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + BS - 1) / BS);
@@ -962,6 +1106,12 @@ static hipError_t launch_chain_m(const LookupArgs &a, hipStream_t s, unsigned ld
 template <int R>
 static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
+    if (a.rec_nr) {   // RC_LAYOUT_RECORDS (bf16, 4 levels: checked by the C-ABI)
+        if (!bf16 || a.levels != 4) return hipErrorNotSupported;
+        if (a.out_cl) hipLaunchKernelGGL((lookup_records_kernel<R, true>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_records_kernel<R, false>), dim3(nblk), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.shk[0]) {   // RC_LAYOUT_DISPARITY (fp32, NCHW output: checked by the C-ABI)
         if (bf16 || a.out_cl) return hipErrorNotSupported;
         if (a.levels == 4) hipLaunchKernelGGL((lookup_sheared_pair_kernel<R, 4>), dim3(nblk), dim3(256), 0, s, a);

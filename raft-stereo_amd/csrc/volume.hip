@@ -531,6 +531,20 @@ constexpr int kB16BK = 32;                  // d rows per stage
 constexpr int kB16P1 = 256;                 // F1 image pitch: 128 w1
 constexpr int kB16MaxFused = 5;             // levels the ring epilogue writes
 constexpr int kB16DeferStage = 16 * 144;    // deferred epilogue: per-wave bf16 image of 16 rows
+// RC_LAYOUT_RECORDS: a 16-row piece of one wave row's levels 0 and 2 (every
+// w2 of the tile, which spans the whole row) staged in a workgroup-shared
+// bf16 image -- element e of row i at byte 2 (pad + e) of the row's
+// level-0 / level-2 part, zeros outside [0, W) -- from which its waves
+// gather the rows' records.  Sized for W2 <= 320 (rc_rec_count(W2) <= 22:
+// level-0 elements up to 347, level-2 up to 95).
+constexpr int kRecL0Pad = 28, kRecL2Pad = 14;                 // element -pad at byte 0
+constexpr int kRecL0P = 752, kRecL2P = 224;                   // bytes per image row
+constexpr int kRecImg = 16 * (kRecL0P + kRecL2P);             // one wave row's piece image
+constexpr int kRecMaxW2 = 320;
+static_assert(2 * (kRecL0Pad + rec_e0(21) + kRecSlots - kRecL2Slots) <= kRecL0P &&
+                  2 * (kRecL2Pad + rec_e2(21) + kRecL2Slots) <= kRecL2P && kRecL0Pad >= -rec_e0(0) + 2 &&
+                  kRecL2Pad == -rec_e2(0),
+              "records image geometry");
 
 template <int NWN, int FMA>
 struct B16Geom {
@@ -614,7 +628,10 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
     constexpr int LIPW = G::NINS / 2;                             // DMA instructions per loader wave per stage
     static_assert(G::NINS % 2 == 0 && LIPW * (SL - 1) + 2 <= 60, "loader vmcnt budget");
     static_assert(!DEFER || FMA == 4, "deferred epilogue: 4 fragments per wave");
-    __shared__ __attribute__((aligned(16))) char smem[SL * G::SLOT + NC * (DEFER ? kB16DeferStage : G::STB)];
+    constexpr bool REC = (MODE & kModeRecords) != 0;              // RC_LAYOUT_RECORDS
+    static_assert(!REC || DEFER, "records: the deferred epilogue");
+    __shared__ __attribute__((aligned(16)))
+    char smem[SL * G::SLOT + (REC ? 2 * kRecImg : NC * (DEFER ? kB16DeferStage : G::STB))];
     typedef __attribute__((address_space(3))) void lds_void;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int D = a.D, H = a.H, W1 = a.W1, W2 = a.W2;
@@ -768,6 +785,10 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             asm volatile("" ::: "memory");
             issue_next();
         }
+        if constexpr (REC) {   // the compute waves' last-tile records (rec_write / rec_emit)
+#pragma unroll
+            for (int p = 0; p < 9; ++p) __builtin_amdgcn_s_barrier();
+        }
         return;
     }
 
@@ -788,6 +809,7 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
     // is stored when the tile ends, after a lane transpose that gives lane
     // (g, i) the 4 level-2 values of fragment ma = g.
     uint32_t h0[FMA][4][2];
+    uint32_t h2[REC ? 4 : 1][2];                                  // REC: level 2 (bf16 pairs of ma)
     int hrow = 0, hm0 = 0, hn0 = 0;
     // per-lane row offsets of the deferred stores (elements): level-0 piece
     // rows (lane >> 3) and 8 + (lane >> 3), level-2 row (lane & 15)
@@ -827,6 +849,20 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
         } else {
             const float sq = a.sq;
             level0([sq](float x) { return x / sq; });
+        }
+        if constexpr (REC) {
+            // level 2 stays in registers too (lane (g, i): column n0/4 + 4 ma + g
+            // of row 16 nb + i), zero past the level's width: the records'
+            // padding
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                float q[4];
+#pragma unroll
+                for (int ma = 0; ma < 4; ++ma) q[ma] = (n0h >> 2) + 4 * ma + g < (W2 >> 2) ? s2[ma][nb] : 0.0f;
+                h2[nb][0] = pack_bf16x2(q[0], q[1]);
+                h2[nb][1] = pack_bf16x2(q[2], q[3]);
+            }
+            return;
         }
         // (hold runs for DEFER kernels only, which have FMA == 4)
 #pragma unroll
@@ -891,6 +927,69 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             }
         }
     };
+    // REC: piece p of the held tile (rows 16p..16p+15 of this wave row) goes
+    // through the wave row's shared image in two stages a barrier apart:
+    // rec_write -- each wave puts its 64 level-0 and 16 level-2 columns in;
+    // rec_emit -- the wave row's NWN waves gather the rows' records from it,
+    // one 16-B chunk per lane, 128 B per 8 lanes: the piece's records are one
+    // contiguous run of 16 * rec_nr lines, written whole
+    char *const rimg = smem + SL * G::SLOT + wm * kRecImg;
+    auto rec_write = [&](int p) {
+        if (!hact) return;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int g = ln >> 4, i16 = ln & 15;
+        char *r0 = rimg + i16 * kRecL0P, *r2 = rimg + 16 * kRecL0P + i16 * kRecL2P;
+#pragma unroll
+        for (int ma = 0; ma < FMA; ++ma) {
+            const int wb = hn0 + 16 * ma + 4 * g;                 // tiles_n == 1: hn0 is the w2 column
+            uint32_t p0 = h0[ma][p][0], p1 = h0[ma][p][1];
+            const int nv = W2 - wb;                               // valid columns of the four
+            if (nv < 4) {
+                p1 = nv <= 2 ? 0u : (p1 & 0xFFFFu);
+                p0 = nv <= 0 ? 0u : (nv == 1 ? (p0 & 0xFFFFu) : p0);
+            }
+            *reinterpret_cast<uint2 *>(r0 + 2 * (kRecL0Pad + wb)) = uint2{p0, p1};
+            const uint32_t q = h2[p][ma >> 1];
+            *reinterpret_cast<uint16_t *>(r2 + 2 * (kRecL2Pad + (hn0 >> 2) + 4 * ma + g)) =
+                (uint16_t)((ma & 1) ? q >> 16 : q);
+        }
+    };
+    auto rec_emit = [&](int p) {
+        if (!hact) return;
+        int ll = wn * 64 + lane;
+        asm volatile("" : "+v"(ll));                              // recomputed per piece (see store_piece)
+        const int c = ll & 7;                                     // the lane's chunk of every record
+        const int NR = a.rec_nr;
+        const int rows = min(16, W1 - (hm0 + 16 * p));
+        const int J = rows * NR;                                  // records of the piece
+        char *base = static_cast<char *>(a.rec) + ((long long)hrow * W1 + hm0 + 16 * p) * NR * 128 + 16 * c;
+        // dword k of chunk c holds slots 2j, 2j+1 (j = 4c + k): level 2 below
+        // slot 26, level 0 from it -- one part per dword, fixed per lane
+        uint32_t off[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = 4 * c + k;
+            off[k] = 2 * j < kRecL2Slots ? (uint32_t)(16 * kRecL0P + 2 * (kRecL2Pad + rec_e2(0) + 2 * j))
+                                         : (uint32_t)(2 * (kRecL0Pad + rec_e0(0) - kRecL2Slots + 2 * j));
+        }
+        for (int t = ll >> 3; t < J; t += 8 * NWN) {
+            const int row = t / NR, r = t - row * NR;
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool l2 = off[k] >= 16 * kRecL0P;
+                v[k] = *reinterpret_cast<const uint32_t *>(rimg + off[k] + row * (l2 ? kRecL2P : kRecL0P) +
+                                                           (l2 ? 8 * r : 32 * r));
+            }
+            *reinterpret_cast<uint4 *>(base + (long long)t * 128) = uint4{v[0], v[1], v[2], v[3]};
+        }
+    };
+    if constexpr (REC) {
+        // zeros around the rows (element -pad.. and past W): never overwritten
+        for (int o = 16 * (int)(threadIdx.x); o < 2 * kRecImg; o += 16 * 64 * NC)
+            *reinterpret_cast<uint4 *>(smem + SL * G::SLOT + o) = uint4{0u, 0u, 0u, 0u};
+    }
     auto zero_acc = [&]() {
 #pragma unroll
         for (int x = 0; x < FMA; ++x)
@@ -931,7 +1030,13 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
         }
         if constexpr (DEFER && !(MODE & kModeNoStores)) {
             if (held) {
-                if constexpr ((MODE & kModeSpread) != 0) {   // 8 half-pieces, one per stage at nst = 8
+                if constexpr (REC) {   // piece p: image at stage 2p, records at 2p + 1 (nst >= 8: launcher)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        if (st == 2 * p) rec_write(p);
+                        else if (st == 2 * p + 1) rec_emit(p);
+                    }
+                } else if constexpr ((MODE & kModeSpread) != 0) {   // 8 half-pieces, one per stage at nst = 8
 #pragma unroll
                     for (int p = 0; p < 8; ++p)
                         if (((p * nst) >> 3) == st) store_piece(p >> 1, p & 1, (p & 1) + 1);
@@ -960,7 +1065,25 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             }
         }
     }
-    if constexpr (DEFER && !(MODE & kModeNoStores)) {
+    if constexpr (REC) {
+        // the last tile (held: ntile_mine >= 1): 9 barriers, matched by the
+        // loader waves' 9 before they end; the first orders the previous
+        // piece's rec_emit (the loop's last stage) before this rec_write
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            rec_write(p);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            rec_emit(p);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+    } else if constexpr (DEFER && !(MODE & kModeNoStores)) {
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) store_piece(nb);
     }
@@ -1229,6 +1352,21 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     const unsigned n = (unsigned)nwg;
+    if (a.rec) {
+        // RC_LAYOUT_RECORDS: the deferred ring kernel with one tile across
+        // the whole row (NWN = ceil(W2 / 64) waves along w2) and at least
+        // 8 stages per tile (its four pieces take two stages each)
+        const int nwn = (a.W2 + 63) / 64;
+        if (!in_bf16 || !a.pyr_bf16 || nwn < 2 || a.W2 > rc::kRecMaxW2 || (a.D + rc::kB16BK - 1) / rc::kB16BK < 8 ||
+            (long long)a.D * a.H * (a.W1 > a.W2 ? a.W1 : a.W2) * 2 >= (1LL << 30))
+            return hipErrorNotSupported;
+        constexpr int RM = rc::kModeRecords;
+        if (nwn == 5) rc::launch_bf16_ring_n<5, 4, 4, RM, true>(a, s);
+        else if (nwn == 4) rc::launch_bf16_ring_n<4, 4, 4, RM, true>(a, s);
+        else if (nwn == 3) rc::launch_bf16_ring_n<3, 4, 4, RM, true>(a, s);
+        else rc::launch_bf16_ring_n<2, 4, 4, RM, true>(a, s);
+        return hipGetLastError();
+    }
     rc::B16Shape sh = in_bf16 ? rc::bf16_ring_shape(a) : rc::B16Shape{0, 0, false};
 #ifdef RAFTCORR_DEV
     if (const hipError_t e = rc::dev_launch_bf16mma(a, sh, s); e != hipErrorNotSupported) return e;
