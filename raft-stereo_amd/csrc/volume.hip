@@ -546,6 +546,69 @@ static_assert(2 * (kRecL0Pad + rec_e0(21) + kRecSlots - kRecL2Slots) <= kRecL0P 
                   kRecL2Pad == -rec_e2(0),
               "records image geometry");
 
+// RC_LAYOUT_RECORDS: the records of unit u (the 8 pixel rows em0 + 8u ..,
+// image half u & 1 of a wave row's piece image `img`) of the tile held at
+// image row erow, gathered and stored by NL lanes (ll: this lane among them;
+// NL a multiple of 8).  Chunk c = ll & 7 of each record holds slots 8c..8c+7:
+// level 2 (slots < 26) for c < 3, level 0 for c > 3, and for c = 3 slots
+// 24-25 of level 2 then 26-31 of level 0.  Each lane reads dword 0 at A and
+// dwords 1-3 at B, B + 4 (8-B aligned): A, B one part's consecutive bytes
+// for c != 3, the two parts for c = 3 -- three LDS reads per chunk, the same
+// for every lane.  The unit's records are one contiguous run of 8 * rec_nr
+// lines (16 B per lane, 128 B per 8 lanes, written whole).
+template <int MODE, int NL>
+__device__ __forceinline__ void rec_emit_unit(const BuildArgs &a, const char *img, int u, int erow, int em0, int ll) {
+    const int c = ll & 7;
+    const int NR = a.rec_nr, W1 = a.W1;
+    const int w1u = em0 + 8 * u;                                  // the unit's first pixel row
+    const int J = min(8, W1 - w1u) * NR;                          // records of the unit
+    // kModeL2Stores (dev timing only, wrong output): 8 L2-resident rows
+    const long long rrow = (MODE & kModeL2Stores) ? (erow & 7) : erow;
+    char *base = static_cast<char *>(a.rec) + (rrow * W1 + w1u) * NR * 128 + 16 * c;
+    const int hb = 8 * (u & 1);                                   // the unit's first image row
+    const int a2 = 16 * kRecL0P + hb * kRecL2P + 2 * (kRecL2Pad + rec_e2(0));         // level-2 slot 0
+    const int a0 = hb * kRecL0P + 2 * (kRecL0Pad + rec_e0(0) - kRecL2Slots);          // level-0 "slot 0"
+    const bool cl2 = c < 3, cmix = c == 3;
+    const int A0 = (cl2 || cmix ? a2 : a0) + 16 * c, PA = cl2 || cmix ? kRecL2P : kRecL0P;
+    const int mA = cl2 || cmix ? 8 : 32;
+    const int B0 = (cl2 ? a2 : a0) + 16 * c + 4, PB = cl2 ? kRecL2P : kRecL0P, mB = cl2 ? 8 : 32;
+    // record t = (row, r): t advances by S = NL / 8 per step, (row, r) by
+    // (drow, dr) with a carry -- no division in the loop
+    constexpr int S = NL >> 3;
+    const int drow = S / NR, dr = S - drow * NR;
+    int t = ll >> 3;
+    int row = t / NR, r = t - row * NR;
+    constexpr int BT = 2;                                         // records' reads in flight per wait (3: VGPR spills)
+    for (; t < J; t += BT * S) {
+        uint32_t v[BT][4];
+#pragma unroll
+        for (int b = 0; b < BT; ++b) {
+            if (t + b * S < J) {
+                const char *pa = img + A0 + row * PA + r * mA;
+                const char *pb = img + B0 + row * PB + r * mB;
+                v[b][0] = *reinterpret_cast<const uint32_t *>(pa);
+                v[b][1] = *reinterpret_cast<const uint32_t *>(pb);
+                const uint2 w = *reinterpret_cast<const uint2 *>(pb + 4);
+                v[b][2] = w.x;
+                v[b][3] = w.y;
+            }
+            r += dr;
+            row += drow;
+            if (r >= NR) { r -= NR; ++row; }
+        }
+#pragma unroll
+        for (int b = 0; b < BT; ++b) {
+            if (t + b * S < J) {
+                if constexpr ((MODE & kModeRecNoStore) != 0)       // dev timing: gathered, not stored
+                    asm volatile("" ::"v"(v[b][0]), "v"(v[b][1]), "v"(v[b][2]), "v"(v[b][3]));
+                else
+                    *reinterpret_cast<uint4 *>(base + (long long)(t + b * S) * 128) =
+                        uint4{v[b][0], v[b][1], v[b][2], v[b][3]};
+            }
+        }
+    }
+}
+
 template <int NWN, int FMA>
 struct B16Geom {
     static constexpr int NW = 2 * NWN;                              // waves
@@ -630,6 +693,7 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
     static_assert(!DEFER || FMA == 4, "deferred epilogue: 4 fragments per wave");
     constexpr bool REC = (MODE & kModeRecords) != 0;              // RC_LAYOUT_RECORDS
     static_assert(!REC || DEFER, "records: the deferred epilogue");
+    constexpr bool LEMIT = REC && (MODE & kModeRecLoaderEmit) != 0;   // dev: the loader waves emit
     __shared__ __attribute__((aligned(16)))
     char smem[SL * G::SLOT + (REC ? 2 * kRecImg : NC * (DEFER ? kB16DeferStage : G::STB))];
     typedef __attribute__((address_space(3))) void lds_void;
@@ -784,10 +848,40 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             issue_next();
+            if constexpr (LEMIT) {
+                // dev: this loader wave emits its wave row's units -- unit
+                // st - 1 of the tile before (stage st = 1..8), or unit 7 of
+                // the tile two back at stage 0 of 8-stage tiles
+                const int k = gs / nst, st = gs - k * nst;
+                int ek = -1, eu = 0;
+                if (st >= 1 && st <= 8 && k >= 1) { ek = k - 1; eu = st - 1; }
+                else if (st == 0 && nst == 8 && k >= 2) { ek = k - 2; eu = 7; }
+                if (ek >= 0) {
+                    const B16Tile et = tile_at(ek);
+                    if (et.M0 + 64 * lid < W1)
+                        rec_emit_unit<MODE, 64>(a, smem + SL * G::SLOT + lid * kRecImg, eu, et.row,
+                                                et.M0 + 64 * lid, lane);
+                }
+            }
         }
         if constexpr (REC) {   // the compute waves' last-tile records (rec_write / rec_emit)
 #pragma unroll
-            for (int p = 0; p < 9; ++p) __builtin_amdgcn_s_barrier();
+            for (int u = 0; u <= 8; ++u) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                if constexpr (LEMIT) {
+                    int ek = -1, eu = 0;
+                    if (u == 0 && nst == 8 && ntile_mine >= 2) { ek = ntile_mine - 2; eu = 7; }
+                    else if (u >= 1) { ek = ntile_mine - 1; eu = u - 1; }
+                    if (ek >= 0) {
+                        const B16Tile et = tile_at(ek);
+                        if (et.M0 + 64 * lid < W1)
+                            rec_emit_unit<MODE, 64>(a, smem + SL * G::SLOT + lid * kRecImg, eu, et.row,
+                                                    et.M0 + 64 * lid, lane);
+                    }
+                }
+            }
         }
         return;
     }
@@ -851,14 +945,23 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             level0([sq](float x) { return x / sq; });
         }
         if constexpr (REC) {
-            // level 2 stays in registers too (lane (g, i): column n0/4 + 4 ma + g
-            // of row 16 nb + i), zero past the level's width: the records'
-            // padding
+            // level 2 stays in registers too, transposed like the row
+            // layout's stores below: lane (g, i) holds columns n0/4 + 4g ..
+            // + 3 of row 16 nb + i (one 8-B image write per unit), zero past
+            // the level's width (the records' padding)
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) {
+                uint32_t R0 = __builtin_bit_cast(uint32_t, s2[0][nb]), R1 = __builtin_bit_cast(uint32_t, s2[1][nb]);
+                uint32_t R2 = __builtin_bit_cast(uint32_t, s2[2][nb]), R3 = __builtin_bit_cast(uint32_t, s2[3][nb]);
+                auto t02 = __builtin_amdgcn_permlane32_swap(R0, R2, false, false);
+                auto t13 = __builtin_amdgcn_permlane32_swap(R1, R3, false, false);
+                auto t01 = __builtin_amdgcn_permlane16_swap(t02[0], t13[0], false, false);
+                auto t23 = __builtin_amdgcn_permlane16_swap(t02[1], t13[1], false, false);
+                const uint32_t qu[4] = {(uint32_t)t01[0], (uint32_t)t01[1], (uint32_t)t23[0], (uint32_t)t23[1]};
                 float q[4];
 #pragma unroll
-                for (int ma = 0; ma < 4; ++ma) q[ma] = (n0h >> 2) + 4 * ma + g < (W2 >> 2) ? s2[ma][nb] : 0.0f;
+                for (int j = 0; j < 4; ++j)
+                    q[j] = (n0h >> 2) + 4 * g + j < (W2 >> 2) ? __builtin_bit_cast(float, qu[j]) : 0.0f;
                 h2[nb][0] = pack_bf16x2(q[0], q[1]);
                 h2[nb][1] = pack_bf16x2(q[2], q[3]);
             }
@@ -927,18 +1030,29 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             }
         }
     };
-    // REC: piece p of the held tile (rows 16p..16p+15 of this wave row) goes
-    // through the wave row's shared image in two stages a barrier apart:
-    // rec_write -- each wave puts its 64 level-0 and 16 level-2 columns in;
-    // rec_emit -- the wave row's NWN waves gather the rows' records from it,
-    // one 16-B chunk per lane, 128 B per 8 lanes: the piece's records are one
-    // contiguous run of 16 * rec_nr lines, written whole
+    // REC: the held tile's rows go out in 8 units of 8 rows (unit u = rows
+    // 8u..8u+7 of this wave row, in half u & 1 of the wave row's shared
+    // 16-row image), one unit per stage of the next tile's K loop, each in two
+    // steps a barrier apart:
+    // rec_write(u) -- at stage u each wave puts its 64 level-0 and 16 level-2
+    //   columns of the unit's rows in;
+    // rec_emit(u) -- at stage u + 1 the wave row's NWN waves gather the rows'
+    //   records from it, one 16-B chunk per lane, 128 B per 8 lanes: the
+    //   unit's records are one contiguous run of 8 * rec_nr lines, written
+    //   whole.
+    // Stage s then emits unit s - 1 from one half while unit s goes into the
+    // other, so every stage carries half a piece of stores (the same stores
+    // in bursts of a whole piece every other stage: +0.35 ms at config 3).
+    // Unit 7 is emitted at stage 8, or at the next tile's stage 0 (pending)
+    // when the tile has exactly 8 stages.
     char *const rimg = smem + SL * G::SLOT + wm * kRecImg;
-    auto rec_write = [&](int p) {
+    auto rec_write = [&](int u) {
         if (!hact) return;
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int g = ln >> 4, i16 = ln & 15;
+        if ((i16 >> 3) != (u & 1)) return;                        // this lane's row is in the other half
+        const int p = u >> 1;
         char *r0 = rimg + i16 * kRecL0P, *r2 = rimg + 16 * kRecL0P + i16 * kRecL2P;
 #pragma unroll
         for (int ma = 0; ma < FMA; ++ma) {
@@ -950,41 +1064,22 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
                 p0 = nv <= 0 ? 0u : (nv == 1 ? (p0 & 0xFFFFu) : p0);
             }
             *reinterpret_cast<uint2 *>(r0 + 2 * (kRecL0Pad + wb)) = uint2{p0, p1};
-            const uint32_t q = h2[p][ma >> 1];
-            *reinterpret_cast<uint16_t *>(r2 + 2 * (kRecL2Pad + (hn0 >> 2) + 4 * ma + g)) =
-                (uint16_t)((ma & 1) ? q >> 16 : q);
         }
+        // level-2 columns n0/4 + 4g .. + 3 (4-B aligned: two dwords)
+        uint32_t *d2 = reinterpret_cast<uint32_t *>(r2 + 2 * (kRecL2Pad + (hn0 >> 2) + 4 * g));
+        d2[0] = h2[p][0];
+        d2[1] = h2[p][1];
     };
-    auto rec_emit = [&](int p) {
-        if (!hact) return;
+    // unit u of the tile held at (erow, em0): its image half -> its records
+    auto rec_emit = [&](int u, int erow, int em0, bool eact) {
+        if (!eact) return;
         int ll = wn * 64 + lane;
-        asm volatile("" : "+v"(ll));                              // recomputed per piece (see store_piece)
-        const int c = ll & 7;                                     // the lane's chunk of every record
-        const int NR = a.rec_nr;
-        const int rows = min(16, W1 - (hm0 + 16 * p));
-        const int J = rows * NR;                                  // records of the piece
-        char *base = static_cast<char *>(a.rec) + ((long long)hrow * W1 + hm0 + 16 * p) * NR * 128 + 16 * c;
-        // dword k of chunk c holds slots 2j, 2j+1 (j = 4c + k): level 2 below
-        // slot 26, level 0 from it -- one part per dword, fixed per lane
-        uint32_t off[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int j = 4 * c + k;
-            off[k] = 2 * j < kRecL2Slots ? (uint32_t)(16 * kRecL0P + 2 * (kRecL2Pad + rec_e2(0) + 2 * j))
-                                         : (uint32_t)(2 * (kRecL0Pad + rec_e0(0) - kRecL2Slots + 2 * j));
-        }
-        for (int t = ll >> 3; t < J; t += 8 * NWN) {
-            const int row = t / NR, r = t - row * NR;
-            uint32_t v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool l2 = off[k] >= 16 * kRecL0P;
-                v[k] = *reinterpret_cast<const uint32_t *>(rimg + off[k] + row * (l2 ? kRecL2P : kRecL0P) +
-                                                           (l2 ? 8 * r : 32 * r));
-            }
-            *reinterpret_cast<uint4 *>(base + (long long)t * 128) = uint4{v[0], v[1], v[2], v[3]};
-        }
+        asm volatile("" : "+v"(ll));                              // recomputed per unit (see store_piece)
+        rec_emit_unit<MODE, 64 * NWN>(a, rimg, u, erow, em0, ll);
     };
+    // the unit 7 that waits for the next tile's stage 0 (8-stage tiles)
+    bool pend = false;
+    int prow = 0, pm0 = 0;
     if constexpr (REC) {
         // zeros around the rows (element -pad.. and past W): never overwritten
         for (int o = 16 * (int)(threadIdx.x); o < 2 * kRecImg; o += 16 * 64 * NC)
@@ -1028,13 +1123,23 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
                 for (int nb = 0; nb < 4; ++nb)
                     acc[ma][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ma], fb[nb], acc[ma][nb], 0, 0, 0);
         }
+        if constexpr (REC && !(MODE & (kModeNoStores | kModeRecNoEmit | kModeRecLoaderEmit))) {
+            if (pend && st == 0) {   // unit 7 of the tile held before the current one
+                rec_emit(7, prow, pm0, true);
+                pend = false;
+            }
+        }
         if constexpr (DEFER && !(MODE & kModeNoStores)) {
             if (held) {
-                if constexpr (REC) {   // piece p: image at stage 2p, records at 2p + 1 (nst >= 8: launcher)
+                if constexpr (REC) {   // unit u: image at stage u, records at u + 1 (nst >= 8: launcher)
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        if (st == 2 * p) rec_write(p);
-                        else if (st == 2 * p + 1) rec_emit(p);
+                    for (int u = 0; u <= 8; ++u) {
+                        if (st == u) {
+                            if constexpr (!(MODE & (kModeRecNoEmit | kModeRecLoaderEmit))) {
+                                if (u >= 1) rec_emit(u - 1, hrow, hm0, hact);
+                            }
+                            if (u < 8) rec_write(u);
+                        }
                     }
                 } else if constexpr ((MODE & kModeSpread) != 0) {   // 8 half-pieces, one per stage at nst = 8
 #pragma unroll
@@ -1053,6 +1158,13 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
             }
         }
         if (++st == nst) {
+            if constexpr (REC) {   // 8-stage tiles: the held tile's unit 7 goes out at the next stage 0
+                if (held && nst == 8 && hact) {
+                    pend = true;
+                    prow = hrow;
+                    pm0 = hm0;
+                }
+            }
             if constexpr (DEFER) hold(cur.row, m0, n0, active);
             else if (active) epilogue_swapped<FMA, MODE, NLM>(acc, a, cur.row, m0, n0, lane, stg);
             st = 0;
@@ -1067,21 +1179,21 @@ __global__ __launch_bounds__(128 * NWN + 128) void build_bf16_ring_kernel(BuildA
     }
     if constexpr (REC) {
         // the last tile (held: ntile_mine >= 1): 9 barriers, matched by the
-        // loader waves' 9 before they end; the first orders the previous
-        // piece's rec_emit (the loop's last stage) before this rec_write
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
+        // loader waves' 9 before they end.  Barrier u orders stage u - 1's
+        // image writes before unit u - 1's gather and unit u - 2's gather
+        // before unit u's writes into the same half.
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            rec_write(p);
+        for (int u = 0; u <= 8; ++u) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            rec_emit(p);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
+            if constexpr (!(MODE & (kModeRecNoEmit | kModeNoStores | kModeRecLoaderEmit))) {
+                if (u == 0 && pend) rec_emit(7, prow, pm0, true);
+                if (u >= 1) rec_emit(u - 1, hrow, hm0, hact);
+            }
+            if constexpr (!(MODE & kModeNoStores)) {
+                if (u < 8) rec_write(u);
+            }
         }
     } else if constexpr (DEFER && !(MODE & kModeNoStores)) {
 #pragma unroll
@@ -1361,6 +1473,9 @@ hipError_t rc_launch_build_bf16mma(rc::BuildArgs &a, int in_bf16, hipStream_t s)
             (long long)a.D * a.H * (a.W1 > a.W2 ? a.W1 : a.W2) * 2 >= (1LL << 30))
             return hipErrorNotSupported;
         constexpr int RM = rc::kModeRecords;
+#ifdef RAFTCORR_DEV
+        if (const hipError_t e = rc::dev_launch_records(a, nwn, s); e != hipErrorNotSupported) return e;
+#endif
         if (nwn == 5) rc::launch_bf16_ring_n<5, 4, 4, RM, true>(a, s);
         else if (nwn == 4) rc::launch_bf16_ring_n<4, 4, 4, RM, true>(a, s);
         else if (nwn == 3) rc::launch_bf16_ring_n<3, 4, 4, RM, true>(a, s);
