@@ -893,11 +893,12 @@ __global__ __launch_bounds__(256) void lookup_sheared_pair_kernel(LookupArgs a) 
 // and finish_pair runs unchanged, so the output is the row layout's bit for
 // bit.
 
-// issue_pair over a record: level-lo element e sits in slot e - e_first + slot_first
+// issue_pair over a record: level-lo element e sits in slot e - e_first + slot_first.
+// plan_record_pair fills the span's window fields and returns the first
+// chunk's slot (cb, a multiple of 8) and which of the NC chunks the taps read.
 template <int R>
-__device__ __forceinline__ void issue_record_pair(PairSpan<R, true> &ps, const LookupArgs &a, int lo, float x,
-                                                  const __amdgpu_buffer_rsrc_t &rs, uint32_t rbyte, int e_first,
-                                                  int slot_first) {
+__device__ __forceinline__ int plan_record_pair(PairSpan<R, true> &ps, const LookupArgs &a, int lo, float x,
+                                                int e_first, int slot_first, uint32_t &okmask) {
     typedef PairSpan<R, true> PS;
     const int Wlo = a.W[lo], Whi = a.W[lo + 1];
     const float xlo = x / (float)(1 << lo), xhi = x / (float)(2 << lo);
@@ -918,14 +919,56 @@ __device__ __forceinline__ void issue_record_pair(PairSpan<R, true> &ps, const L
     const int cb = sslot >= 0 ? sslot & ~7 : -((-sslot + 7) & ~7);      // chunk base (floor to 8)
     ps.sh = sslot - cb;
     const int slo = lo_e - e_first + slot_first, shi = hi_e - e_first + slot_first;
+    okmask = 0;
 #pragma unroll
     for (int k = 0; k < PS::NC; ++k) {
         const int cs = cb + 8 * k;
-        const bool ok = lo_e <= hi_e && cs <= shi && cs + 7 >= slo && cs >= 0 && cs + 8 <= kRecSlots;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (int)(rbyte + 2u * (uint32_t)cs) : (int)0xFFFFFF00u,
-                                                             0, 0);
+        if (lo_e <= hi_e && cs <= shi && cs + 7 >= slo && cs >= 0 && cs + 8 <= kRecSlots) okmask |= 1u << k;
+    }
+    return cb;
+}
+
+template <int R, bool NOLOAD = false>
+__device__ __forceinline__ void issue_record_pair(PairSpan<R, true> &ps, const LookupArgs &a, int lo, float x,
+                                                  const __amdgpu_buffer_rsrc_t &rs, uint32_t rbyte, int e_first,
+                                                  int slot_first) {
+    typedef PairSpan<R, true> PS;
+    uint32_t okm;
+    const int cb = plan_record_pair<R>(ps, a, lo, x, e_first, slot_first, okm);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) ps.q[k][c] = v[c];
+    for (int k = 0; k < PS::NC; ++k) {
+        const int cs = cb + 8 * k;
+        const bool ok = (okm >> k) & 1u;
+        if constexpr (NOLOAD) {   // dev timing: the addresses, not the loads
+            uint32_t o = ok ? rbyte + 2u * (uint32_t)cs : 0u;
+            asm volatile("" : "+v"(o));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) ps.q[k][c] = o + c;
+        } else {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+                rs, ok ? (int)(rbyte + 2u * (uint32_t)cs) : (int)0xFFFFFF00u, 0, 0);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) ps.q[k][c] = v[c];
+        }
+    }
+}
+
+// The same chunks from the pixel's whole record staged in LDS (COOP).
+template <int R>
+__device__ __forceinline__ void lds_record_pair(PairSpan<R, true> &ps, const LookupArgs &a, int lo, float x,
+                                                const char *rec, int e_first, int slot_first) {
+    typedef PairSpan<R, true> PS;
+    uint32_t okm;
+    const int cb = plan_record_pair<R>(ps, a, lo, x, e_first, slot_first, okm);
+#pragma unroll
+    for (int k = 0; k < PS::NC; ++k) {
+        const int cs = cb + 8 * k;
+        uint4 v = uint4{0u, 0u, 0u, 0u};
+        if ((okm >> k) & 1u) v = *reinterpret_cast<const uint4 *>(rec + 2 * cs);
+        ps.q[k][0] = v.x;
+        ps.q[k][1] = v.y;
+        ps.q[k][2] = v.z;
+        ps.q[k][3] = v.w;
     }
 }
 
@@ -972,8 +1015,14 @@ __device__ __forceinline__ void record_taps_mem(const LookupArgs &a, const uint1
 }
 
 // CL: channels-last output (RC_OUT_CHANNELS_LAST) through the per-wave LDS
-// tile of lookup_pair_kernel; else NCHW dword stores.
-template <int R, bool CL>
+// tile of lookup_pair_kernel; else NCHW dword stores.  M: dev timing modes
+// (libraftcorr_dev.so, wrong output): 1 no output stores, 2 no record loads,
+// 3 record loads only (no tap math, no stores).
+// COOP: each wave's 64 records are fetched whole, eight 128-B lines per
+// buffer_load ... lds instruction (lane L: record 8k + L/8, 16-B chunk L % 8)
+// into a per-wave LDS image, then each lane reads its chunks from there:
+// 8 line requests per instruction instead of 64 partial ones.
+template <int R, bool CL, int M = 0, bool COOP = false>
 __global__ __launch_bounds__(256) void lookup_records_kernel(LookupArgs a) {
     constexpr int NL = 4, C = NL * (2 * R + 1);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -988,11 +1037,43 @@ __global__ __launch_bounds__(256) void lookup_records_kernel(LookupArgs a) {
     const auto rs = make_rsrc(blkrec, clamp_bytes((a.P - q.pblk) * (long long)NR * kRecSlots * 2));
     const uint32_t rbyte = (uint32_t)((q.lrow * NR + r) * kRecSlots * 2);
     PairSpan<R, true> sp[2];
-    issue_record_pair<R>(sp[0], a, 0, q.x, rs, rbyte, rec_e0(r), kRecL2Slots);
-    issue_record_pair<R>(sp[1], a, 2, q.x, rs, rbyte, rec_e2(r), 0);
-    __shared__ __attribute__((aligned(16))) float ctile[CL ? 4 * 64 * C : 1];
+    // per wave: the staged records (8 KB), then the channels-last tile
+    // (64 C floats, 9 KB at R = 4) in the same bytes once they are read
+    constexpr int WB = (COOP && 64 * C * 4 < 8192) ? 8192 : 64 * C * 4;
+    __shared__ __attribute__((aligned(16))) char lds[(CL || COOP) ? 4 * WB : 16];
+    char *wlds = lds + (threadIdx.x >> 6) * WB;
+    if constexpr (COOP) {
+        typedef __attribute__((address_space(3))) void lds_void;
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            // record of pixel 8k + lane/8 of this wave, its chunk lane % 8
+            const uint32_t rb = (uint32_t)__shfl((int)rbyte, 8 * k + (lane >> 3), 64);
+            const int wp = (int)(threadIdx.x & ~63) + 8 * k + (lane >> 3);
+            const uint32_t off = q.pblk + wp < a.P ? rb + 16u * (uint32_t)(lane & 7) : 0xFFFFFF00u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(wlds + 1024 * k), 16, (int)off, 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const char *myrec = wlds + 128 * lane;
+        lds_record_pair<R>(sp[0], a, 0, q.x, myrec, rec_e0(r), kRecL2Slots);
+        lds_record_pair<R>(sp[1], a, 2, q.x, myrec, rec_e2(r), 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // all reads done before the tile reuses the bytes
+    } else {
+        issue_record_pair<R, M == 2>(sp[0], a, 0, q.x, rs, rbyte, rec_e0(r), kRecL2Slots);
+        issue_record_pair<R, M == 2>(sp[1], a, 2, q.x, rs, rbyte, rec_e2(r), 0);
+    }
+    if constexpr (M == 3) {   // dev: the loads alone
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int j = 0; j < PairSpan<R, true>::NC; ++j) acc ^= sp[k].q[j][0] ^ sp[k].q[j][1] ^ sp[k].q[j][2] ^ sp[k].q[j][3];
+        asm volatile("" ::"v"(acc));
+        return;
+    }
+    float *const ctw = reinterpret_cast<float *>(wlds);       // this wave's channels-last tile
     auto sink = [&](int ch, float v) {
-        if constexpr (CL) ctile[(threadIdx.x >> 6) * 64 * C + (threadIdx.x & 63) * C + ch] = v;
+        if constexpr (CL) ctw[(threadIdx.x & 63) * C + ch] = v;
         else if (q.active) q.outp[(long long)ch * a.HW] = v;
     };
 #pragma unroll
@@ -1006,14 +1087,16 @@ __global__ __launch_bounds__(256) void lookup_records_kernel(LookupArgs a) {
     if constexpr (CL) {
         const int lane = threadIdx.x & 63;
         const long long pw = q.pblk + (threadIdx.x & ~63);
-        const float *t = ctile + (threadIdx.x >> 6) * 64 * C;
+        const float *t = ctw;
         const long long lim = (a.P - pw < 64 ? a.P - pw : 64) * C;
 #pragma unroll
         for (int k = 0; k < (16 * C + 63) / 64; ++k) {
             const int e = (k * 64 + lane) * 4;
             if (e >= 64 * C || e >= lim) continue;
             const f32x4 v = *reinterpret_cast<const f32x4 *>(t + e);
-            if (e + 4 <= lim) {
+            if constexpr (M == 1) {   // dev: no output stores
+                asm volatile("" ::"v"(v));
+            } else if (e + 4 <= lim) {
                 *reinterpret_cast<f32x4 *>(a.out + pw * C + e) = v;
             } else {
 #pragma unroll
@@ -1108,6 +1191,9 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + 255) / 256);
     if (a.rec_nr) {   // RC_LAYOUT_RECORDS (bf16, 4 levels: checked by the C-ABI)
         if (!bf16 || a.levels != 4) return hipErrorNotSupported;
+#ifdef RAFTCORR_DEV
+        if (const hipError_t e = dev_launch_records<R>(a, s); e != hipErrorNotSupported) return e;
+#endif
         if (a.out_cl) hipLaunchKernelGGL((lookup_records_kernel<R, true>), dim3(nblk), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((lookup_records_kernel<R, false>), dim3(nblk), dim3(256), 0, s, a);
         return hipGetLastError();
