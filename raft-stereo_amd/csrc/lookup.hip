@@ -1015,15 +1015,16 @@ __device__ __forceinline__ void record_taps_mem(const LookupArgs &a, const uint1
 }
 
 // CL: channels-last output (RC_OUT_CHANNELS_LAST) through the per-wave LDS
-// tile of lookup_pair_kernel; else NCHW dword stores.  M: dev timing modes
+// tile of lookup_pair_kernel; else NCHW dword stores.  COOP (the product)
+// see below; without it each lane loads its own chunks (the dev A/B).  M: dev timing modes
 // (libraftcorr_dev.so, wrong output): 1 no output stores, 2 no record loads,
 // 3 record loads only (no tap math, no stores).
 // COOP: each wave's 64 records are fetched whole, eight 128-B lines per
 // buffer_load ... lds instruction (lane L: record 8k + L/8, 16-B chunk L % 8)
 // into a per-wave LDS image, then each lane reads its chunks from there:
 // 8 line requests per instruction instead of 64 partial ones.
-template <int R, bool CL, int M = 0, bool COOP = false>
-__global__ __launch_bounds__(256) void lookup_records_kernel(LookupArgs a) {
+template <int R, bool CL, int M = 0, bool COOP = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void lookup_records_kernel(LookupArgs a) {
     constexpr int NL = 4, C = NL * (2 * R + 1);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const PairPixel q = pair_pixel<R, NL>(a, (long long)blk * 256);
@@ -1039,8 +1040,8 @@ __global__ __launch_bounds__(256) void lookup_records_kernel(LookupArgs a) {
     PairSpan<R, true> sp[2];
     // per wave: the staged records (8 KB), then the channels-last tile
     // (64 C floats, 9 KB at R = 4) in the same bytes once they are read
-    constexpr int WB = (COOP && 64 * C * 4 < 8192) ? 8192 : 64 * C * 4;
-    __shared__ __attribute__((aligned(16))) char lds[(CL || COOP) ? 4 * WB : 16];
+    constexpr int WB = CL ? (COOP && 64 * C * 4 < 8192 ? 8192 : 64 * C * 4) : (COOP ? 8192 : 16);
+    __shared__ __attribute__((aligned(16))) char lds[4 * WB];
     char *wlds = lds + (threadIdx.x >> 6) * WB;
     if constexpr (COOP) {
         typedef __attribute__((address_space(3))) void lds_void;
@@ -1194,8 +1195,10 @@ static hipError_t launch_pair_r(const LookupArgs &a, int bf16, hipStream_t s) {
 #ifdef RAFTCORR_DEV
         if (const hipError_t e = dev_launch_records<R>(a, s); e != hipErrorNotSupported) return e;
 #endif
-        if (a.out_cl) hipLaunchKernelGGL((lookup_records_kernel<R, true>), dim3(nblk), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((lookup_records_kernel<R, false>), dim3(nblk), dim3(256), 0, s, a);
+        // the cooperative whole-record fetch: 118.4 vs 121.5 us per config-3
+        // lookup (interleaved, bit-identical; profiles/r06/rec_o)
+        if (a.out_cl) hipLaunchKernelGGL((lookup_records_kernel<R, true, 0, true>), dim3(nblk), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((lookup_records_kernel<R, false, 0, true>), dim3(nblk), dim3(256), 0, s, a);
         return hipGetLastError();
     }
     if (a.shk[0]) {   // RC_LAYOUT_DISPARITY (fp32, NCHW output: checked by the C-ABI)
