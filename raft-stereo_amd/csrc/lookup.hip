@@ -1108,6 +1108,104 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// One 64-pixel group of the record lookup: pixels, records, fetch offset.
+struct RecGroup {
+    PairPixel q;
+    int r;
+    const uint16_t *blkrec;
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t rbyte;
+};
+
+// Two 64-pixel groups per wave (dev A/B, RAFTCORR_REC_LOOKUP=10/11): both
+// groups' records are fetched cooperatively up front, so the second group's
+// lines are in flight while the first group's taps are computed; block b
+// covers pixels [512b, 512b + 512), wave w groups w and w + 4.  LDS per wave:
+// 9 KB (group A's records, then each group's channels-last tile) + 8 KB
+// (group B's records): two blocks per CU.
+template <int R, bool CL>
+__global__ __launch_bounds__(256) void lookup_records2_kernel(LookupArgs a) {
+    constexpr int NL = 4, C = NL * (2 * R + 1);
+    constexpr int TB = CL && 64 * C * 4 > 8192 ? 64 * C * 4 : 8192;
+    __shared__ __attribute__((aligned(16))) char lds[4 * (TB + 8192)];
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int lane = threadIdx.x & 63;
+    char *bufA = lds + (threadIdx.x >> 6) * (TB + 8192), *bufB = bufA + TB;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int NR = a.rec_nr;
+    auto setup = [&](long long pblk) {
+        RecGroup g;
+        g.q = pair_pixel<R, NL>(a, pblk);
+        float mf = floorf(g.q.x / 2.0f);
+        mf = fminf(fmaxf(mf, (float)kRecM0), (float)(kRecM0 + 8 * NR - 1));
+        g.r = ((int)mf - kRecM0) >> 3;
+        g.blkrec = static_cast<const uint16_t *>(a.lvl[0]) + g.q.pblk * (long long)NR * kRecSlots;
+        g.rs = make_rsrc(g.blkrec, clamp_bytes((a.P - g.q.pblk) * (long long)NR * kRecSlots * 2));
+        g.rbyte = (uint32_t)((g.q.lrow * NR + g.r) * kRecSlots * 2);
+        return g;
+    };
+    auto fetch = [&](const RecGroup &g, char *buf) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t rb = (uint32_t)__shfl((int)g.rbyte, 8 * k + (lane >> 3), 64);
+            const int wp = (int)(threadIdx.x & ~63) + 8 * k + (lane >> 3);
+            const uint32_t off = g.q.pblk + wp < a.P ? rb + 16u * (uint32_t)(lane & 7) : 0xFFFFFF00u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(g.rs, (lds_void *)(buf + 1024 * k), 16, (int)off, 0, 0, 0);
+        }
+    };
+    // the group's taps from its staged records; CL: into the tile at bufA
+    auto compute = [&](const RecGroup &g, const char *recbuf) {
+        PairSpan<R, true> sp[2];
+        const char *myrec = recbuf + 128 * lane;
+        lds_record_pair<R>(sp[0], a, 0, g.q.x, myrec, rec_e0(g.r), kRecL2Slots);
+        lds_record_pair<R>(sp[1], a, 2, g.q.x, myrec, rec_e2(g.r), 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        float *const ctw = reinterpret_cast<float *>(bufA);
+        auto sink = [&](int ch, float v) {
+            if constexpr (CL) ctw[lane * C + ch] = v;
+            else if (g.q.active) g.q.outp[(long long)ch * a.HW] = v;
+        };
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (__builtin_expect(sp[k].inwin && !sp[k].valid, 0)) {
+                record_taps_mem<R>(a, g.blkrec + g.q.lrow * (long long)NR * kRecSlots, 2 * k, g.q.x, sink);
+                continue;
+            }
+            finish_pair<R, true, true>(sp[k], a, 2 * k, g.q.x, g.q.pp, sink);
+        }
+    };
+    auto store_tile = [&](const RecGroup &g) {
+        if constexpr (CL) {
+            const long long pw = g.q.pblk + (threadIdx.x & ~63);
+            const float *t = reinterpret_cast<const float *>(bufA);
+            const long long lim = (a.P - pw < 64 ? a.P - pw : 64) * C;
+#pragma unroll
+            for (int k = 0; k < (16 * C + 63) / 64; ++k) {
+                const int e = (k * 64 + lane) * 4;
+                if (e >= 64 * C || e >= lim) continue;
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(t + e);
+                if (e + 4 <= lim) {
+                    *reinterpret_cast<f32x4 *>(a.out + pw * C + e) = v;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (e + j < lim) a.out[pw * C + e + j] = v[j];
+                }
+            }
+        }
+    };
+    const RecGroup ga = setup((long long)blk * 512), gb = setup((long long)blk * 512 + 256);
+    fetch(ga, bufA);
+    fetch(gb, bufB);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");            // group A's 8 DMA landed
+    compute(ga, bufA);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // group B's (and, NCHW, A's stores)
+    store_tile(ga);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // tile A read: bufA free again
+    compute(gb, bufB);
+    store_tile(gb);
+}
+
 template <int R, int NL, bool BF16, bool EXACT, int BS = 256, int WPE = 1>
 static void launch_k(const LookupArgs &a, hipStream_t s) {
     const unsigned nblk = (unsigned)((a.P + BS - 1) / BS);

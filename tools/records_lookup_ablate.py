@@ -2,7 +2,8 @@
 32-launch sequences at the KITTI config of the record lookup and its
 dev-library timing modes (RAFTCORR_REC_LOOKUP: 1 no output stores, 2 no
 record loads, 3 record loads only, 4 the cooperative whole-record fetch
-into LDS, 5 / 6 that without output stores / loads only).
+into LDS (the product since r06o), 5 / 6 that without output stores / loads
+only, 9 per-lane chunk loads, 10 two 64-pixel groups per wave).
 
     python tools/records_lookup_ablate.py [--reps 5] [--batch B]
 """
@@ -35,16 +36,17 @@ def main():
     with torch.no_grad(), _lib.dev_library():
         f1, f2, cs = bench.make_inputs((B, D, H, W1, W2, L, r, iters, None), dev, seed=1, dtype=torch.bfloat16)
         blk = CorrBlock1D(f1, f2, num_levels=L, radius=r, channels_last=True, layout="records")
-        # the cooperative fetch (mode 4) returns the product's output bit for bit
+        # the cooperative variants (modes 4, 10) return the product's output bit for bit
         from test_corr_gpu import special_coords
         g = torch.Generator().manual_seed(7)
         same4 = True
         for c in (cs[0], special_coords(B, H, W1, W2, g).to(dev)):
             os.environ["RAFTCORR_REC_LOOKUP"] = "0"
             ref = blk(c).clone()
-            os.environ["RAFTCORR_REC_LOOKUP"] = "4"
-            got = blk(c)
-            same4 &= bool(torch.equal(ref.contiguous().view(torch.int32), got.contiguous().view(torch.int32)))
+            for m in ("4", "10"):
+                os.environ["RAFTCORR_REC_LOOKUP"] = m
+                got = blk(c)
+                same4 &= bool(torch.equal(ref.contiguous().view(torch.int32), got.contiguous().view(torch.int32)))
         for _ in range(a.reps):
             for m in modes:
                 os.environ["RAFTCORR_REC_LOOKUP"] = str(m)
