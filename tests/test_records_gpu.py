@@ -30,6 +30,7 @@ SHAPES = [
     (1, 256, 3, 150, 150, 3),
     (1, 256, 3, 150, 150, 2),
     (1, 256, 3, 150, 150, 1),
+    (2, 256, 1, 40, 130, 4),        # W1 < 64: the second wave row of every tile idle
 ]
 
 
