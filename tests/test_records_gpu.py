@@ -169,3 +169,21 @@ def test_records_refusals():
         rc = lib.rc_corr_lookup_chain(ptrs, widths, lds, dt, 4, 4, c.data_ptr(), 2 * 130, 1, 2, 130,
                                       out.data_ptr(), None)
         assert rc in (_lib.RC_EUNSUPPORTED, _lib.RC_EINVAL), dt
+
+
+def test_records_config3_fullsize_bit_identical():
+    """BASELINE config 3 at its per-GPU size (B = 64, 94 x 311 fmaps): the
+    records (5.27 GB, past 4 GiB: the build stores through 64-bit addresses,
+    the lookup addresses each block's records from its own base) against the
+    shadowed rows, on the bench field and the special coordinates."""
+    B, D, H, W1, W2, r = 64, 256, 94, 311, 311, 4
+    f1, f2, g = fmaps(B, D, H, W1, W2, 5100)
+    with torch.no_grad():
+        rows = CorrBlock1D(f1, f2, num_levels=4, radius=r, channels_last=True)
+        rec = CorrBlock1D(f1, f2, num_levels=4, radius=r, channels_last=True, layout="records")
+        assert rec._records.numel() * 2 > 4 << 30
+        bench_field = torch.cat([torch.arange(W1).float().view(1, 1, 1, W1) - torch.rand(B, 1, H, W1, generator=g) * 64,
+                                 torch.zeros(B, 1, H, W1)], 1)
+        for c in (bench_field, edge_coords(B, H, W1, W2, g)):
+            c = c.to(DEV)
+            assert torch.equal(bits(rows(c)), bits(rec(c)))
