@@ -531,12 +531,13 @@ constexpr int kB16BK = 32;                  // d rows per stage
 constexpr int kB16P1 = 256;                 // F1 image pitch: 128 w1
 constexpr int kB16MaxFused = 5;             // levels the ring epilogue writes
 constexpr int kB16DeferStage = 16 * 144;    // deferred epilogue: per-wave bf16 image of 16 rows
-// RC_LAYOUT_RECORDS: a 16-row piece of one wave row's levels 0 and 2 (every
-// w2 of the tile, which spans the whole row) staged in a workgroup-shared
-// bf16 image -- element e of row i at byte 2 (pad + e) of the row's
-// level-0 / level-2 part, zeros outside [0, W) -- from which its waves
-// gather the rows' records.  Sized for W2 <= 320 (rc_rec_count(W2) <= 22:
-// level-0 elements up to 347, level-2 up to 95).
+// RC_LAYOUT_RECORDS: 16 rows of one wave row's levels 0 and 2 (every w2 of
+// the tile, which spans the whole row) staged in a workgroup-shared bf16
+// image -- element e of row i at byte 2 (pad + e) of the row's level-0 /
+// level-2 part, zeros outside [0, W) -- as two halves of 8 rows, one being
+// written while the wave row gathers the other's records.  Sized for
+// W2 <= 320 (RC_REC_COUNT(W2) <= 22: level-0 elements up to 347, level-2 up
+// to 95).
 constexpr int kRecL0Pad = 28, kRecL2Pad = 14;                 // element -pad at byte 0
 constexpr int kRecL0P = 752, kRecL2P = 224;                   // bytes per image row
 constexpr int kRecImg = 16 * (kRecL0P + kRecL2P);             // one wave row's piece image
@@ -556,6 +557,8 @@ static_assert(2 * (kRecL0Pad + rec_e0(21) + kRecSlots - kRecL2Slots) <= kRecL0P 
 // for c != 3, the two parts for c = 3 -- three LDS reads per chunk, the same
 // for every lane.  The unit's records are one contiguous run of 8 * rec_nr
 // lines (16 B per lane, 128 B per 8 lanes, written whole).
+typedef unsigned rec_u32x4 __attribute__((ext_vector_type(4)));
+
 template <int MODE, int NL>
 __device__ __forceinline__ void rec_emit_unit(const BuildArgs &a, const char *img, int u, int erow, int em0, int ll) {
     const int c = ll & 7;
@@ -601,6 +604,9 @@ __device__ __forceinline__ void rec_emit_unit(const BuildArgs &a, const char *im
             if (t + b * S < J) {
                 if constexpr ((MODE & kModeRecNoStore) != 0)       // dev timing: gathered, not stored
                     asm volatile("" ::"v"(v[b][0]), "v"(v[b][1]), "v"(v[b][2]), "v"(v[b][3]));
+                else if constexpr ((MODE & kModeRecNT) != 0)       // dev A/B: streaming (non-temporal) stores
+                    __builtin_nontemporal_store(rec_u32x4{v[b][0], v[b][1], v[b][2], v[b][3]},
+                                                reinterpret_cast<rec_u32x4 *>(base + (long long)(t + b * S) * 128));
                 else
                     *reinterpret_cast<uint4 *>(base + (long long)(t + b * S) * 128) =
                         uint4{v[b][0], v[b][1], v[b][2], v[b][3]};

@@ -2,7 +2,7 @@
 timings at the KITTI config of the row build (shadowed levels 0 and 2), the
 record build, and the dev-library ablations of the record build
 (RAFTCORR_REC_MODE: 1 records gathered not stored, 2 stored into 8
-L2-resident image rows, 3 piece images only, 4 neither, 5 the loader waves gather and store).
+L2-resident image rows, 3 piece images only, 4 neither, 5 the loader waves gather and store, 6 non-temporal record stores).
 
     python tools/records_build_ablate.py [--reps 7] [--batch B]
 """
@@ -29,16 +29,16 @@ def main():
     B = a.batch or B
     dev = torch.device("cuda", 0)
     variants = [("rows", "rows", 0), ("records", "records", 0)] + \
-        [(f"rec_mode{m}", "records", m) for m in (1, 2, 3, 4, 5)]
+        [(f"rec_mode{m}", "records", m) for m in (1, 2, 3, 4, 5, 6)]
     t = {n: [] for n, _, _ in variants}
     with torch.no_grad(), _lib.dev_library():
         f1, f2, _ = bench.make_inputs((B, D, H, W1, W2, L, r, 1, None), dev, seed=1, dtype=torch.bfloat16)
         # the loader-emission variant writes the product's records
         recs = {}
-        for mode in (0, 5):
+        for mode in (0, 5, 6):
             os.environ["RAFTCORR_REC_MODE"] = str(mode)
             recs[mode] = CorrBlock1D(f1, f2, num_levels=L, radius=r, layout="records")._records
-        same5 = bool(torch.equal(recs[0].view(torch.int16), recs[5].view(torch.int16)))
+        same5 = all(bool(torch.equal(recs[0].view(torch.int16), recs[m].view(torch.int16))) for m in (5, 6))
         del recs
         for _ in range(a.reps):
             for name, lay, mode in variants:
@@ -52,7 +52,7 @@ def main():
                 t[name].append(e[0].elapsed_time(e[1]) * 1e3)
                 del blk
         os.environ.pop("RAFTCORR_REC_MODE", None)
-    print(json.dumps({"B": B, "mode5_records_equal": same5, "build_us": {n: statistics.median(v) for n, v in t.items()},
+    print(json.dumps({"B": B, "modes5_6_records_equal": same5, "build_us": {n: statistics.median(v) for n, v in t.items()},
                       "min_us": {n: min(v) for n, v in t.items()}}), flush=True)
 
 
