@@ -118,3 +118,30 @@ def test_records_flag_validation():
     assert chain(ptrs, RB | _lib.shadow_level(0)) == _lib.RC_EUNSUPPORTED
     assert chain(_lib.ptr_array([f(0x1000), None, f(0x4000), None]), RB) == _lib.RC_EINVAL
     assert chain(ptrs, RB, lv=2) == _lib.RC_EUNSUPPORTED
+
+
+@pytest.mark.parametrize("W2", [65, 130, 240, 311, 320])
+def test_records_level_gathers_the_documented_geometry(W2):
+    """corr.records_level (the corr_pyramid gather of layout="records") on a
+    CPU tensor laid out by the header's definition, written here directly:
+    record r, slot s < 26 = level-2 element 4r - 14 + s, slot s >= 26 =
+    level-0 element 16r - 26 + (s - 26), zeros off the row."""
+    import torch
+    from raft_stereo_amd import corr as rcorr
+    P, NR = 5, _lib.rec_count(W2)
+    g = torch.Generator().manual_seed(W2)
+    l0 = torch.randn(P, W2, generator=g).to(torch.bfloat16)
+    l2 = torch.randn(P, W2 >> 2, generator=g).to(torch.bfloat16)
+    rec = torch.zeros(P, NR, 64, dtype=torch.bfloat16)
+    for r in range(NR):
+        for s in range(64):
+            if s < 26:
+                e, src, W = rec_e2(r) + s, l2, W2 >> 2
+            else:
+                e, src, W = rec_e0(r) + s - 26, l0, W2
+            if 0 <= e < W:
+                rec[:, r, s] = src[:, e]
+    got0 = rcorr.records_level(rec, 0, W2).reshape(P, -1)
+    got2 = rcorr.records_level(rec, 2, W2).reshape(P, -1)
+    assert torch.equal(got0.view(torch.int16), l0.view(torch.int16))
+    assert torch.equal(got2.view(torch.int16), l2.view(torch.int16))
