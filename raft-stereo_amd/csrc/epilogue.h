@@ -16,7 +16,8 @@ enum { kModeNoLoads = 1, kModeNoStores = 2, kModeNoMath = 4, kModeAlignedSrc = 8
        kModePackedSub = 8192,
        kModeL2Stores = 65536, kModeDirect = 131072, kModeFastEpi = 262144, kModeGenericEpi = 524288,
        kModePairEpi = 1048576, kModeRecords = 1 << 23, kModeRecNoStore = 1 << 24, kModeRecNoEmit = 1 << 25,
-       kModeRecLoaderEmit = 1 << 26, kModeRecNT = 1 << 27 };
+       kModeRecLoaderEmit = 1 << 26, kModeRecNT = 1 << 27,
+       kModePhasePrio = 1 << 28, kModeMfmaPrio = 1 << 29 };
 
 // VW consecutive level values -> memory (fp32, or bf16 rounded to nearest even).
 template <int VW>

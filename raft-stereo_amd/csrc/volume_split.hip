@@ -137,11 +137,36 @@ __device__ __forceinline__ void split_body(const SpCtx &c, const BuildArgs &a, c
             SplitFrag fb[FB];
 #pragma unroll
             for (int n = 0; n < FB; ++n) fb[n] = sp_read<MODE, TW>(pb + 64 * n);
+            if constexpr ((MODE & kModePhasePrio) != 0) {
+                // dev A/B: every fragment read and split first, then all the
+                // MFMAs at raised wave priority, so that the SIMD's other wave
+                // fills the issue slots with its split while these run
+                SplitFrag fa[FA];
 #pragma unroll
-            for (int m = 0; m < FA; ++m) {
-                const SplitFrag fa = sp_read<MODE, TW>(pa + 64 * m);
+                for (int m = 0; m < FA; ++m) fa[m] = sp_read<MODE, TW>(pa + 64 * m);
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(3);
 #pragma unroll
-                for (int n = 0; n < FB; ++n) mma6(acc[m][n], fa, fb[n]);
+                for (int m = 0; m < FA; ++m)
+#pragma unroll
+                    for (int n = 0; n < FB; ++n) mma6(acc[m][n], fa[m], fb[n]);
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(0);
+            } else {
+#pragma unroll
+                for (int m = 0; m < FA; ++m) {
+                    const SplitFrag fa = sp_read<MODE, TW>(pa + 64 * m);
+                    if constexpr ((MODE & kModeMfmaPrio) != 0) {   // dev A/B: each fragment's MFMAs at raised priority
+                        __builtin_amdgcn_sched_barrier(0);
+                        __builtin_amdgcn_s_setprio(3);
+                    }
+#pragma unroll
+                    for (int n = 0; n < FB; ++n) mma6(acc[m][n], fa, fb[n]);
+                    if constexpr ((MODE & kModeMfmaPrio) != 0) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        __builtin_amdgcn_s_setprio(0);
+                    }
+                }
             }
         }
     }
