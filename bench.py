@@ -601,11 +601,12 @@ def main():
     ap.add_argument("--shadow", default="default",
                     help="pyramid levels with an RC_SHADOW copy: 'default' (per-shape rule, "
                          "corr.default_shadow_levels), 'none', or a comma list such as 0,2")
-    ap.add_argument("--layout", default=None, choices=("rows", "disparity", "records"),
+    ap.add_argument("--layout", default=None, choices=("rows", "disparity", "records", "auto"),
                     help="CorrBlock1D pyramid layout: the reference's rows (default for the fp32 "
                          "configs), the opt-in disparity-major levels (RC_LAYOUT_DISPARITY, DESIGN.md "
-                         "§3.2h) or the bf16 record layout (RC_LAYOUT_RECORDS, §3.2i; default for "
-                         "kitti, where it shortens the step by 6-10 %%)")
+                         "§3.2h), the bf16 record layout (RC_LAYOUT_RECORDS, §3.2i) or auto (default "
+                         "for kitti: records once the bf16 level 0 exceeds the 256 MiB Infinity Cache, "
+                         "i.e. per-GPU batch >= 16; 10 %% shorter steps at batch 64)")
     ap.add_argument("--field", default="random", choices=FIELDS,
                     help="coords field: random (SURVEY §8d, the headline), smooth or slant (coherent)")
     ap.add_argument("--network", action="store_true",
@@ -620,8 +621,8 @@ def main():
     args = ap.parse_args()
     if args.channels_last is None:   # NHWC output where it goes to HBM (the bf16 config)
         args.channels_last = args.config in BF16_CONFIGS
-    if args.layout is None:          # one line per pixel per lookup for the bf16 pyramid
-        args.layout = "records" if args.config in BF16_CONFIGS else "rows"
+    if args.layout is None:          # the record layout where it pays (bf16, level 0 past the MALL)
+        args.layout = "auto" if args.config in BF16_CONFIGS else "rows"
     if args.network and args.config != "middlebury":
         ap.error("--network applies to --config middlebury")
     shadow = (None if args.shadow == "default" else () if args.shadow == "none"
@@ -853,8 +854,8 @@ def main():
         roof_volume["mfma_util_pmc"] = vpmc["mfma_util"]
     lgbs = lbytes / (lookup_launch_ms * 1e-3) / 1e9
     pair = blk._chain and (L == 2 or (L == 4 and 2 in written))
-    lfamily = ("rc::lookup_sheared_pair_kernel" if args.layout == "disparity"
-               else "rc::lookup_records_kernel" if args.layout == "records"
+    lfamily = ("rc::lookup_sheared_pair_kernel" if blk.layout == "disparity"
+               else "rc::lookup_records_kernel" if blk.layout == "records"
                else "rc::lookup_pair_kernel" if pair else "rc::lookup_chain_kernel" if blk._chain
                else "rc::lookup_levelpar_kernel" if P < 65536 and L <= 4 else "rc::lookup_kernel")
     lname, lpmc = pmc_entry(pmc, lfamily)
@@ -902,7 +903,7 @@ def main():
                    "fmap": [B, D, H, W1], "W2": W2, "levels": L, "radius": r, "iters": iters,
                    "parallelism": (f"row-shard x{world}" if row_shard else f"batch-shard x{world}"),
                    "corr_out_layout": "channels_last" if args.channels_last else "nchw",
-                   "pyramid_layout": args.layout, "coords_field": args.field},
+                   "pyramid_layout": blk.layout, "coords_field": args.field},
         "roofline": dominant,
         "roofline_volume": roof_volume,
         "roofline_lookup": roof_lookup,
@@ -915,12 +916,12 @@ def main():
         "notes": (f"disparity-major block (layout='disparity', RC_LAYOUT_DISPARITY): the build writes "
                   f"levels {written} as S[b,h][k][w1], k = (w1 >> l) - j + W_l - 1 (the same values and "
                   "bytes as the rows), the lookup reads them with the disparity-major pair kernel; "
-                  "corr_pyramid is gathered into rows only when read" if args.layout == "disparity" else
+                  "corr_pyramid is gathered into rows only when read" if blk.layout == "disparity" else
                   f"record block (layout='records', RC_LAYOUT_RECORDS): the build writes levels {written} "
                   f"as {_lib.rec_count(W2)} 128-B records per pixel row (the rows' values, 1.8x the "
                   "shadowed rows' bytes; the extra writes are in the build's time, not in its "
                   "algorithmic bytes), each lookup reads one line per pixel; corr_pyramid is "
-                  "gathered into rows only when read" if args.layout == "records" else
+                  "gathered into rows only when read" if blk.layout == "records" else
                   f"pool-chain block: the build writes pyramid levels {written} (levels "
                   f"{sorted(blk._shadow)} also as a half-line-shifted RC_SHADOW copy: those "
                   "writes are in the build's time, not in its algorithmic bytes); every lookup "

@@ -464,6 +464,20 @@ def records_supported(fmap1, fmap2, num_levels, radius, pyramid_dtype):
     return None
 
 
+def auto_layout(fmap1, fmap2, num_levels, radius, pyramid_dtype=None, lazy_levels=None, shadow=None,
+                low_latency=False, grad_shadow=None, exact_f32=False):
+    """CorrBlock1D(layout="auto"): "records" for a bf16 pyramid the record
+    build serves (with the default options) whose level 0 exceeds the
+    256 MiB Infinity Cache, else "rows" (DESIGN.md §3.2i)."""
+    if pyramid_dtype is None:
+        pyramid_dtype = torch.bfloat16 if fmap1.dtype in (torch.bfloat16, torch.float16) else torch.float32
+    if (low_latency or shadow or grad_shadow or exact_f32 or lazy_levels is False
+            or records_supported(fmap1, fmap2, num_levels, radius, pyramid_dtype) is not None):
+        return "rows"
+    B, D, H, W1, W2 = _check_fmaps(fmap1, fmap2)
+    return "records" if B * H * W1 * W2 * 2 > (256 << 20) else "rows"
+
+
 def build_records(fmap1, fmap2):
     """rc_corr_build with RC_LAYOUT_RECORDS: a (B*H*W1, rec_count(W2), 64)
     bf16 tensor.  fp32/fp16 fmaps are rounded to bf16 first (round to nearest
@@ -875,8 +889,16 @@ class CorrBlock1D:
         # bf16 pair layout's levels 0 and 2 as 128-B records, one line per
         # pixel per lookup instead of two; the same values and lookups bit for
         # bit; the build writes 1.8x the bytes of the shadowed rows.
+        # layout="auto": the records where they pay -- a bf16 pyramid the
+        # record build serves whose level 0 no longer fits the 256 MiB
+        # Infinity Cache (config 3: step 5.31 vs 6.00 ms at B = 64, 1.50 vs
+        # 1.64 at B = 16; at B = 8, 145 MB, the rows win: 0.835 vs 0.898,
+        # profiles/r06/z, za) -- else the rows.
+        if layout == "auto":
+            layout = auto_layout(fmap1, fmap2, num_levels, radius, pyramid_dtype, lazy_levels, shadow,
+                                 low_latency, grad_shadow, exact_f32)
         if layout not in ("rows", "disparity", "records"):
-            raise ValueError(f"CorrBlock1D: layout={layout!r}: 'rows', 'disparity' or 'records'")
+            raise ValueError(f"CorrBlock1D: layout={layout!r}: 'rows', 'disparity', 'records' or 'auto'")
         self.layout = layout
         self._sheared = None
         self._records = None

@@ -187,3 +187,21 @@ def test_records_config3_fullsize_bit_identical():
         for c in (bench_field, edge_coords(B, H, W1, W2, g)):
             c = c.to(DEV)
             assert torch.equal(bits(rows(c)), bits(rec(c)))
+
+
+def test_auto_layout_rule():
+    """layout="auto": the records for a bf16 pyramid the record build serves
+    once its level 0 exceeds the 256 MiB Infinity Cache (config 3 per-GPU
+    batch >= 16), the rows otherwise (profiles/r06/z, za)."""
+    def z(B, D, H, W, dt=torch.bfloat16):
+        return torch.zeros(B, D, H, W, dtype=dt, device=DEV)
+    assert rcorr.auto_layout(z(16, 256, 94, 311), z(16, 256, 94, 311), 4, 4) == "records"
+    assert rcorr.auto_layout(z(8, 256, 94, 311), z(8, 256, 94, 311), 4, 4) == "rows"       # 145 MB
+    assert rcorr.auto_layout(z(16, 256, 94, 311, torch.float32), z(16, 256, 94, 311, torch.float32), 4, 4) == "rows"
+    assert rcorr.auto_layout(z(16, 256, 94, 311), z(16, 256, 94, 311), 4, 4, shadow=True) == "rows"
+    assert rcorr.auto_layout(z(4, 256, 94, 400), z(4, 256, 94, 400), 4, 4) == "rows"       # W2 > 320
+    with torch.no_grad():
+        f = z(16, 256, 94, 311)
+        assert CorrBlock1D(f, f, num_levels=4, radius=4, layout="auto").layout == "records"
+        g = z(2, 256, 8, 311)
+        assert CorrBlock1D(g, g, num_levels=4, radius=4, layout="auto").layout == "rows"
