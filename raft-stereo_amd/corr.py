@@ -1148,7 +1148,6 @@ class CorrBlock1D:
         if B * H * W1 == 0:
             return corr, new, flow
         if self._records is not None:
-            keep = self._records
             ptrs, widths, lds = _records_args(self._records, self._shape[3])
             dt = _lib.RC_BF16 | _lib.RC_LAYOUT_RECORDS
         elif self._chain:
